@@ -1,0 +1,360 @@
+#!/usr/bin/env python3
+"""Device-resident batched Snappy benchmark (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3-decompress]
+
+One "step" = one pass of the hot path over one batch resident in HBM.
+Default workload (the north-star target config): decompress
+65,536 x 64 KiB Zipf-text bodies.  Other workloads: c2-decompress (65,536 x
+4 KiB random), c3-compress, cm-decompress (power-law 256 B..1 MiB), c5-compress.
+
+For N > 1 launch with torch.distributed.run; each rank owns its own shard of
+messages (weak scaling, no data-path collective: messages are independent).
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "flare-cpp_amd" / "py"))
+
+import fsg  # noqa: E402
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+WORKLOADS = {
+    # name: (op, kind, n_msgs, size spec, description)
+    "c3-decompress": ("decompress", fsg.KIND_TEXT, 65536, 65536,
+                      "C3 decompress: 65,536 x 64 KiB Zipf-text bodies (~2.0x), device-resident"),
+    "c2-decompress": ("decompress", fsg.KIND_RANDOM, 65536, 4096,
+                      "C2 decompress: 65,536 x 4 KiB random bodies, device-resident"),
+    "c3-compress": ("compress", fsg.KIND_TEXT, 65536, 65536,
+                    "C3 compress: 65,536 x 64 KiB Zipf-text bodies, device-resident"),
+    "cm-decompress": ("decompress", fsg.KIND_MIXED, 1 << 20, "mixed",
+                      "CM decompress: 1,048,576 power-law bodies 256 B..1 MiB, 1 in 4 random"),
+    "c5-compress": ("compress", fsg.KIND_PROTO, 262144, "mixed",
+                    "C5 compress: 262,144 synthetic SnappyMessageProto responses"),
+}
+
+
+def kernel_source_hash() -> str:
+    h = hashlib.sha256()
+    for p in sorted((REPO / "flare-cpp_amd" / "csrc").glob("*")):
+        h.update(p.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c3-decompress", choices=sorted(WORKLOADS))
+    ap.add_argument("--n-msgs", type=int, default=0, help="override messages per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--verify-sample", type=int, default=64)
+    return ap.parse_args()
+
+
+def build_inputs(kind, n, size_spec, first_index):
+    if size_spec == "mixed":
+        # shard r of the CM/C5 size stream: regenerate the stream prefix and slice
+        sizes = fsg.mixed_sizes(first_index + n)[first_index:]
+    else:
+        sizes = np.full(n, size_spec, dtype=np.uint32)
+    return fsg.make_batch(kind, sizes, first_index=first_index)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    codec = fsg.SnappyGPU(local)
+
+    op, kind, n_default, size_spec, desc = WORKLOADS[args.workload]
+    n = args.n_msgs or n_default
+    first = rank * n  # weak scaling: each rank owns messages [rank*n, (rank+1)*n)
+    t_gen = time.time()
+    batch = build_inputs(kind, n, size_spec, first)
+    raw_total = batch.total
+
+    def H(a):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+    d_raw = H(batch.data)
+    d_raw_off, d_raw_len = H(batch.offsets), H(batch.lens)
+    caps = np.array([fsg.max_compressed_length(int(x)) for x in batch.lens], dtype=np.uint64)
+    c_off, c_tot = fsg.slot_offsets(caps)
+    d_comp = torch.zeros(c_tot, dtype=torch.uint8, device=dev)
+    d_comp_off = H(c_off)
+    d_comp_len = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_status = torch.zeros(n, dtype=torch.int32, device=dev)
+    max_len = int(batch.lens.max())
+    # Compressed inputs come from the GPU encoder (checked against the oracle below).
+    codec.compress(d_raw, d_raw_off, d_raw_len, n, max_len, d_comp, d_comp_off, d_comp_len, d_status)
+    torch.cuda.synchronize()
+    comp_len = d_comp_len.cpu().numpy().view(np.uint32).copy()
+    comp_total = int(comp_len.astype(np.uint64).sum())
+    errors = int((d_status != 0).sum().item())
+
+    # Oracle spot check of the compressed bytes (checker only, never timed).
+    sample_ok = None
+    if args.verify_sample > 0:
+        sys.path.insert(0, str(REPO / "oracle"))
+        from bind import Oracle
+        orc = Oracle()
+        idx = np.linspace(0, n - 1, min(n, args.verify_sample)).astype(np.int64)
+        host_comp = d_comp.cpu().numpy()
+        sample_ok = all(
+            host_comp[int(c_off[i]):int(c_off[i]) + int(comp_len[i])].tobytes() == orc.compress(batch.item(int(i)))
+            for i in idx)
+
+    # Decode output slots (exact uncompressed sizes) -- laid out like the raw batch.
+    d_out = torch.zeros(max(raw_total, 1), dtype=torch.uint8, device=dev)
+    d_out_len = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_cap = d_raw_len
+    d_comp_len_u = d_comp_len  # int32 view is fine: lengths < 2^31
+    stream = torch.cuda.current_stream()
+
+    if op == "decompress":
+        def step():
+            codec.decompress(d_comp, d_comp_off, d_comp_len_u, n, d_out, d_raw_off, d_cap, d_out_len,
+                             d_status, stream=stream)
+        algo_bytes = raw_total + comp_total  # each input byte read once, each output byte written once
+    else:
+        def step():
+            codec.compress(d_raw, d_raw_off, d_raw_len, n, max_len, d_comp, d_comp_off, d_comp_len,
+                           d_status, stream=stream)
+        algo_bytes = raw_total + comp_total
+    gen_s = time.time() - t_gen
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for k in range(args.steps):
+        step()
+        evs[k + 1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)]
+    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+
+    # Correctness of the timed output (device-side, untimed).
+    if op == "decompress":
+        errors += int((d_status != 0).sum().item())
+        roundtrip_ok = bool(torch.equal(d_out[:raw_total], d_raw[:raw_total]))
+    else:
+        errors += int((d_status != 0).sum().item())
+        roundtrip_ok = bool((d_comp_len.cpu().numpy().view(np.uint32) == comp_len).all())
+
+    t_step = wall / args.steps
+    if world > 1:
+        t = torch.tensor([t_step, avg_kernel_s], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_step, avg_kernel_s = float(t[0]), float(t[1])
+        s = torch.tensor([raw_total, comp_total, errors, int(not roundtrip_ok)], dtype=torch.int64, device=dev)
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        raw_all, comp_all, errors, bad = (int(x) for x in s.tolist())
+        roundtrip_ok = bad == 0
+    else:
+        raw_all, comp_all = raw_total, comp_total
+
+    # End-to-end (host pinned -> device -> kernel -> host pinned), untimed in `value`.
+    e2e = None
+    if not args.no_e2e and rank == 0:
+        e2e = end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp_total, n,
+                         max_len, dev)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(op, batch, d_comp, c_off, comp_len, args.cpu_threads)
+
+    if rank == 0:
+        value = raw_all / t_step / GIB
+        achieved = algo_bytes / avg_kernel_s / 1e9
+        pmc = load_traffic(args.workload)
+        line = {
+            "metric": "GiB/s device-resident Snappy decode+encode, batched RPC bodies, 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "GiB/s (uncompressed bytes)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_step * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64-seeded bodies, SURVEY.md §8(d)); compressed by the GPU "
+                    "encoder, byte-checked against the oracle",
+            "config": {
+                "workload": desc,
+                "op": op,
+                "messages_per_gpu": n,
+                "global_batch": n * world,
+                "raw_bytes_per_gpu": raw_total,
+                "compressed_bytes_per_gpu": comp_total,
+                "ratio": round(raw_total / max(1, comp_total), 4),
+                "parallelism": f"shard{world} (messages by index, no data-path collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": pmc.get("traffic_bytes_per_launch") if pmc else None,
+                "algorithmic_bytes_per_launch": algo_bytes,
+                "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
+                "read_frac": round((comp_total if op == "decompress" else raw_total) / avg_kernel_s / 1e9
+                                   / HBM_PEAK_GBS, 4),
+            },
+            "cpu_baseline": cpu,
+            "end_to_end": e2e,
+            "correct": {"status_errors": errors, "roundtrip_ok": roundtrip_ok, "oracle_sample_ok": sample_ok},
+            "kernel_src": kernel_source_hash(),
+            "setup_s": round(gen_s, 2),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def load_traffic(workload: str):
+    p = REPO / "profiles" / f"pmc_{workload}.json"
+    if not p.exists():
+        return None
+    d = json.loads(p.read_text())
+    return d if d.get("kernel_src") == kernel_source_hash() else None
+
+
+def end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp_total, n, max_len, dev):
+    """Pinned host -> HBM -> kernel -> pinned host, one pass (reported in DESIGN.md)."""
+    stream = torch.cuda.current_stream()
+    if op == "decompress":
+        h_in = torch.empty(d_comp.numel(), dtype=torch.uint8, pin_memory=True)
+        h_in.copy_(d_comp.cpu())
+        h_out = torch.empty(raw_total, dtype=torch.uint8, pin_memory=True)
+        d_in = torch.empty_like(d_comp)
+        d_out = torch.empty(raw_total, dtype=torch.uint8, device=dev)
+        in_bytes, out_bytes = comp_total, raw_total
+    else:
+        h_in = torch.from_numpy(batch.data).pin_memory()
+        h_out = torch.empty(d_comp.numel(), dtype=torch.uint8, pin_memory=True)
+        d_in = torch.empty(h_in.numel(), dtype=torch.uint8, device=dev)
+        d_out = torch.empty_like(d_comp)
+        in_bytes, out_bytes = raw_total, comp_total
+    d_off_in = torch.from_numpy(c_off if op == "decompress" else batch.offsets).to(dev)
+    d_len_in = torch.from_numpy((comp_len if op == "decompress" else batch.lens).view(np.int32)).to(dev)
+    d_off_out = torch.from_numpy(batch.offsets if op == "decompress" else c_off).to(dev)
+    d_cap = torch.from_numpy(batch.lens.view(np.int32)).to(dev)
+    d_ol = torch.empty(n, dtype=torch.int32, device=dev)
+    d_st = torch.empty(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(2):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        e[0].record(stream)
+        d_in.copy_(h_in, non_blocking=True)
+        e[1].record(stream)
+        if op == "decompress":
+            codec.decompress(d_in, d_off_in, d_len_in, n, d_out, d_off_out, d_cap, d_ol, d_st, stream=stream)
+        else:
+            codec.compress(d_in, d_off_in, d_len_in, n, max_len, d_out, d_off_out, d_ol, d_st, stream=stream)
+        e[2].record(stream)
+        h_out.copy_(d_out[:h_out.numel()], non_blocking=True)
+        e[3].record(stream)
+        torch.cuda.synchronize()
+        ms = [e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2]), e[2].elapsed_time(e[3])]
+        if best is None or sum(ms) < sum(best):
+            best = ms
+    tot = sum(best) / 1e3
+    return {
+        "gib_s_uncompressed": round(raw_total / tot / GIB, 3),
+        "h2d_ms": round(best[0], 3), "kernel_ms": round(best[1], 3), "d2h_ms": round(best[2], 3),
+        "h2d_gb_s": round(in_bytes / (best[0] / 1e3) / 1e9, 2),
+        "d2h_gb_s": round(out_bytes / (best[2] / 1e3) / 1e9, 2),
+        "note": "serial pinned hipMemcpyAsync H2D + kernel + D2H on one stream, no overlap",
+    }
+
+
+def cpu_baseline(op, batch, d_comp, c_off, comp_len, threads):
+    """The reference's own CPU Snappy (oracle/_ref, per-message Source/Sink path with
+    8160-byte cord_buf fragments) on a bounded sample of the same workload, timed on
+    this host's cores.  Falls back to the C restatement ("port") if _ref is absent."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    from bind import Oracle, Reference
+    nthreads = threads or max(1, min(16, len(os.sched_getaffinity(0))))
+    n = len(batch)
+    per_msg = batch.total / max(1, n)
+    # bounded sample: ~1 GiB of decode work or ~0.25 GiB of encode work per pass
+    target = (1 << 30) if op == "decompress" else (1 << 28)
+    m = int(max(1, min(n, target // max(1, per_msg))))
+    lens = batch.lens[:m].copy()
+    offs = batch.offsets[:m].copy()
+    host_comp = d_comp[: int(c_off[m - 1] + comp_len[m - 1]) + 1].cpu().numpy()
+    clen = comp_len[:m].copy()
+    coff = c_off[:m].copy()
+    kind = "reference" if Reference.available() else "port"
+    eng = Reference() if kind == "reference" else Oracle()
+    out_len = np.zeros(m, np.uint32)
+    if op == "decompress":
+        out = np.zeros(max(1, int(lens.astype(np.uint64).sum())), np.uint8)
+        if kind == "reference":
+            dt = eng.batch(1, host_comp, coff, clen, out, offs, lens, out_len, nthreads)
+        else:
+            st = np.zeros(m, np.int32)
+            dt = eng.uncompress_batch(host_comp, coff, clen, out, offs, lens, out_len, st, nthreads)
+        ok = bool(np.array_equal(out[: int(lens.astype(np.uint64).sum())], batch.data[: int(lens.astype(np.uint64).sum())]))
+    else:
+        caps = np.array([fsg.max_compressed_length(int(x)) for x in lens], np.uint64)
+        oo, tot = fsg.slot_offsets(caps)
+        out = np.zeros(tot, np.uint8)
+        if kind == "reference":
+            dt = eng.batch(0, batch.data, offs, lens, out, oo, None, out_len, nthreads)
+        else:
+            dt = eng.compress_batch(batch.data, offs, lens, out, oo, out_len, nthreads)
+        ok = bool(np.array_equal(out_len, clen))
+    raw = int(lens.astype(np.uint64).sum())
+    return {
+        "value": round(raw / dt / GIB, 3),
+        "unit": "GiB/s (uncompressed bytes)",
+        "cores": nthreads,
+        "kind": kind,
+        "sample": f"first {m} messages of the same batch ({raw / GIB:.3f} GiB raw), {op}, "
+                  f"{nthreads} threads x strided messages, 8160-B fragments; wall {dt:.3f} s; "
+                  f"output equal to GPU's: {ok}",
+    }
+
+
+if __name__ == "__main__":
+    main()

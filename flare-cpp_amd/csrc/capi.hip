@@ -1,0 +1,117 @@
+// capi.hip -- extern "C" boundary of libflare_snappy_gpu.so.
+// Declarations and the reference interface each call replaces:
+// include/flare_snappy_gpu.h.
+#include <cstdio>
+#include <cstring>
+
+#include "../../include/flare_snappy_gpu.h"
+#include "snappy_device.h"
+
+namespace fsg {
+hipError_t launch_decode(const u8* in, const u64* in_off, const u32* in_len,
+                         u32 n_msgs, u8* out, const u64* out_off,
+                         const u32* out_cap, u32* out_len, i32* status,
+                         u32 flags, hipStream_t stream);
+hipError_t launch_headers(const u8* in, const u64* in_off, const u32* in_len,
+                          u32 n_msgs, u32* ulen, int lenient, hipStream_t stream);
+hipError_t launch_encode(const u8* in, const u64* in_off, const u32* in_len,
+                         u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
+                         u32* out_len, i32* status, hipStream_t stream);
+}  // namespace fsg
+
+namespace {
+thread_local char g_err[256] = "";
+
+int record(hipError_t e, const char* where) {
+  if (e == hipSuccess) return FSG_SUCCESS;
+  snprintf(g_err, sizeof(g_err), "%s: %s", where, hipGetErrorString(e));
+  return FSG_ERR_HIP;
+}
+}  // namespace
+
+extern "C" {
+
+const char* fsg_version(void) { return "flare-snappy-gpu 0.1 gfx950"; }
+
+const char* fsg_last_error(void) { return g_err; }
+
+int fsg_init(int device) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) {
+    snprintf(g_err, sizeof(g_err), "fsg_init: no HIP device (%s)",
+             hipGetErrorString(e));
+    return FSG_ERR_NO_DEVICE;
+  }
+  if (device < 0 || device >= n) return FSG_ERR_INVALID_ARG;
+  return record(hipSetDevice(device), "hipSetDevice");
+}
+
+size_t fsg_max_compressed_length(size_t n) { return 32 + n + n / 6; }
+
+int fsg_get_uncompressed_length(const void* compressed, size_t n,
+                                uint32_t* ulen, int lenient) {
+  const uint8_t* p = static_cast<const uint8_t*>(compressed);
+  uint32_t r = 0;
+  for (int i = 0; i < 5; ++i) {
+    if ((size_t)i >= n) return 0;
+    uint32_t c = p[i];
+    r |= (c & 0x7fu) << (7 * i);
+    if (c < 128) {
+      if (!lenient && i == 4 && c >= 16) return 0;  // Parse32WithLimit
+      *ulen = r;
+      return i + 1;
+    }
+  }
+  return 0;
+}
+
+int fsg_uncompressed_lengths_batch(const uint8_t* d_in, const uint64_t* d_in_off,
+                                   const uint32_t* d_in_len, uint32_t n_msgs,
+                                   uint32_t* d_ulen, int lenient, void* stream) {
+  if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_ulen))
+    return FSG_ERR_INVALID_ARG;
+  return record(fsg::launch_headers(d_in, d_in_off, d_in_len, n_msgs, d_ulen,
+                                    lenient, (hipStream_t)stream),
+                "fsg_uncompressed_lengths_batch");
+}
+
+size_t fsg_compress_workspace_bytes(uint32_t, uint64_t) { return 0; }
+size_t fsg_decompress_workspace_bytes(uint32_t, uint64_t) { return 0; }
+
+int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
+                       const uint32_t* d_in_len, uint32_t n_msgs,
+                       uint32_t max_in_len, uint8_t* d_out,
+                       const uint64_t* d_out_off, uint32_t* d_out_len,
+                       int32_t* d_status, void* d_workspace,
+                       size_t workspace_bytes, void* stream) {
+  (void)d_workspace;
+  (void)workspace_bytes;
+  if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off ||
+                 !d_out_len || !d_status))
+    return FSG_ERR_INVALID_ARG;
+  return record(fsg::launch_encode(d_in, d_in_off, d_in_len, n_msgs, max_in_len,
+                                   d_out, d_out_off, d_out_len, d_status,
+                                   (hipStream_t)stream),
+                "fsg_compress_batch");
+}
+
+int fsg_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
+                         const uint32_t* d_in_len, uint32_t n_msgs,
+                         uint8_t* d_out, const uint64_t* d_out_off,
+                         const uint32_t* d_out_cap, uint32_t* d_out_len,
+                         int32_t* d_status, uint32_t flags, void* d_workspace,
+                         size_t workspace_bytes, void* stream) {
+  (void)d_workspace;
+  (void)workspace_bytes;
+  const bool validate = flags & FSG_FLAG_VALIDATE_ONLY;
+  if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out_len || !d_status ||
+                 (!validate && (!d_out || !d_out_off || !d_out_cap))))
+    return FSG_ERR_INVALID_ARG;
+  return record(fsg::launch_decode(d_in, d_in_off, d_in_len, n_msgs, d_out,
+                                   d_out_off, d_out_cap, d_out_len, d_status,
+                                   flags, (hipStream_t)stream),
+                "fsg_decompress_batch");
+}
+
+}  // extern "C"

@@ -1,0 +1,226 @@
+"""ctypes binding of libflare_snappy_gpu.so (include/flare_snappy_gpu.h) and of
+the synthetic-data generator, for the Python test suite and bench.py.
+
+The product path is the C ABI; this module only marshals device pointers
+(torch tensors on cuda:N are used as plain device allocations) and never
+falls back to anything else: if the HIP library is missing, loading raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parents[1]
+LIB_DIR = PKG_DIR / "lib"
+REPO_DIR = PKG_DIR.parent
+HEADER = REPO_DIR / "include" / "flare_snappy_gpu.h"
+
+FSG_OK, FSG_CORRUPT, FSG_BAD_HEADER, FSG_SLOT_TOO_SMALL = 0, 1, 2, 3
+FSG_FLAG_VALIDATE_ONLY, FSG_FLAG_STRICT_HEADER = 1, 2
+
+_c = ctypes
+_vp, _sz, _u32, _u64, _i32 = _c.c_void_p, _c.c_size_t, _c.c_uint32, _c.c_uint64, _c.c_int32
+
+_SIGS = {
+    "fsg_version": (_c.c_char_p, []),
+    "fsg_init": (_c.c_int, [_c.c_int]),
+    "fsg_last_error": (_c.c_char_p, []),
+    "fsg_max_compressed_length": (_sz, [_sz]),
+    "fsg_get_uncompressed_length": (_c.c_int, [_vp, _sz, _c.POINTER(_u32), _c.c_int]),
+    "fsg_uncompressed_lengths_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _c.c_int, _vp]),
+    "fsg_compress_workspace_bytes": (_sz, [_u32, _u64]),
+    "fsg_decompress_workspace_bytes": (_sz, [_u32, _u64]),
+    "fsg_compress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "fsg_decompress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
+}
+
+
+def header_symbols(header: Path = HEADER) -> list[str]:
+    """Every fsg_* function declared in include/flare_snappy_gpu.h."""
+    import re
+    text = header.read_text()
+    return sorted(set(re.findall(r"\b(fsg_[a-z0-9_]+)\s*\(", text)))
+
+
+def load_gpu_lib(path: Path | None = None) -> ctypes.CDLL:
+    path = Path(path or os.environ.get("FSG_LIB", LIB_DIR / "libflare_snappy_gpu.so"))
+    if not path.exists():
+        raise RuntimeError(f"HIP codec library missing: {path} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(str(path))
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    return lib
+
+
+def _ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+class SnappyGPU:
+    """Batched device codec through the C ABI.  Tensors must be on one cuda device."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_gpu_lib()
+        rc = self.lib.fsg_init(device)
+        if rc != 0:
+            raise RuntimeError(f"fsg_init({device}) = {rc}: {self.lib.fsg_last_error().decode()}")
+        self.device = device
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed rc={rc}: {self.lib.fsg_last_error().decode()}")
+
+    @staticmethod
+    def _stream(stream) -> int | None:
+        if stream is None:
+            import torch
+            return torch.cuda.current_stream().cuda_stream
+        return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+    def compress(self, d_in, d_in_off, d_in_len, n, max_in_len, d_out, d_out_off, d_out_len,
+                 d_status, stream=None, workspace=None):
+        ws = 0 if workspace is None else workspace.numel() * workspace.element_size()
+        self._check(self.lib.fsg_compress_batch(
+            _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, max_in_len, _ptr(d_out),
+            _ptr(d_out_off), _ptr(d_out_len), _ptr(d_status), _ptr(workspace), ws,
+            self._stream(stream)), "fsg_compress_batch")
+
+    def decompress(self, d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
+                   d_status, flags=0, stream=None, workspace=None):
+        ws = 0 if workspace is None else workspace.numel() * workspace.element_size()
+        self._check(self.lib.fsg_decompress_batch(
+            _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off),
+            _ptr(d_out_cap), _ptr(d_out_len), _ptr(d_status), flags, _ptr(workspace), ws,
+            self._stream(stream)), "fsg_decompress_batch")
+
+    def uncompressed_lengths(self, d_in, d_in_off, d_in_len, n, d_ulen, lenient=True, stream=None):
+        self._check(self.lib.fsg_uncompressed_lengths_batch(
+            _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_ulen), int(lenient),
+            self._stream(stream)), "fsg_uncompressed_lengths_batch")
+
+
+# ---------------------------------------------------------------------------
+# Batches (host side): one contiguous uint8 buffer + uint64 offsets + uint32 lengths.
+
+class Batch:
+    def __init__(self, data: np.ndarray, offsets: np.ndarray, lens: np.ndarray):
+        self.data = np.ascontiguousarray(data, dtype=np.uint8)
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.lens = np.ascontiguousarray(lens, dtype=np.uint32)
+
+    def __len__(self):
+        return len(self.lens)
+
+    def item(self, i: int) -> bytes:
+        o = int(self.offsets[i])
+        return self.data[o:o + int(self.lens[i])].tobytes()
+
+    @property
+    def total(self) -> int:
+        return int(self.lens.astype(np.uint64).sum())
+
+    @staticmethod
+    def from_list(items) -> "Batch":
+        lens = np.array([len(x) for x in items], dtype=np.uint32)
+        offs = np.zeros(len(items), dtype=np.uint64)
+        if len(items) > 1:
+            offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        data = np.frombuffer(b"".join(items), dtype=np.uint8) if items else np.zeros(0, np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        return Batch(data.copy(), offs, lens)
+
+
+def slot_offsets(caps: np.ndarray, align: int = 16) -> tuple[np.ndarray, int]:
+    """Exclusive prefix offsets of slots of the given capacities, `align`-aligned."""
+    caps = caps.astype(np.uint64)
+    sizes = (caps + np.uint64(align - 1)) // np.uint64(align) * np.uint64(align)
+    offs = np.zeros(len(caps), dtype=np.uint64)
+    if len(caps) > 1:
+        offs[1:] = np.cumsum(sizes[:-1])
+    total = int(sizes.sum()) if len(caps) else 0
+    return offs, max(total, align)
+
+
+def max_compressed_length(n):
+    return 32 + n + n // 6
+
+
+# ---------------------------------------------------------------------------
+# Synthetic data (flare-cpp_amd/tools/datagen.c).
+
+_DG = None
+
+
+def datagen() -> ctypes.CDLL:
+    global _DG
+    if _DG is None:
+        p = LIB_DIR / "libflare_datagen.so"
+        if not p.exists():
+            raise RuntimeError(f"datagen library missing: {p}")
+        lib = ctypes.CDLL(str(p))
+        lib.dg_text_body.argtypes = [_u64, _vp, _sz]
+        lib.dg_random_body.argtypes = [_u64, _vp, _sz]
+        lib.dg_mixed_sizes.argtypes = [_u64, _vp]
+        lib.dg_snappy_message.argtypes = [_u64, _u32, _vp]
+        lib.dg_snappy_message.restype = _sz
+        lib.dg_fnv1a64.argtypes = [_vp, _sz]
+        lib.dg_fnv1a64.restype = _u64
+        lib.dg_fill_batch.argtypes = [_c.c_int, _u64, _u64, _vp, _vp, _vp, _vp, _c.c_int]
+        lib.dg_digest_batch.argtypes = [_vp, _vp, _vp, _u64, _vp]
+        _DG = lib
+    return _DG
+
+
+KIND_TEXT, KIND_RANDOM, KIND_MIXED, KIND_PROTO = 0, 1, 2, 3
+
+
+def _threads() -> int:
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def make_batch(kind: int, sizes, first_index: int = 0, threads: int | None = None) -> Batch:
+    """Generate message bodies first_index.. with the given sizes (for KIND_PROTO the
+    sizes are text lengths and the returned lengths are serialized lengths)."""
+    dg = datagen()
+    sizes = np.ascontiguousarray(np.asarray(sizes, dtype=np.uint32))
+    n = len(sizes)
+    if kind == KIND_PROTO:
+        lens = np.array([dg.dg_snappy_message(first_index + i, int(s), None) for i, s in enumerate(sizes)],
+                        dtype=np.uint32)
+    else:
+        lens = sizes.copy()
+    offs = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    total = int(lens.astype(np.uint64).sum())
+    data = np.zeros(max(total, 1), dtype=np.uint8)
+    out_lens = np.zeros(n, dtype=np.uint32)
+    dg.dg_fill_batch(kind, first_index, n, sizes.ctypes.data, offs.ctypes.data, data.ctypes.data,
+                     out_lens.ctypes.data, threads or _threads())
+    return Batch(data, offs, lens)
+
+
+def mixed_sizes(n: int) -> np.ndarray:
+    s = np.zeros(n, dtype=np.uint32)
+    datagen().dg_mixed_sizes(n, s.ctypes.data)
+    return s
+
+
+def fnv1a64(b: bytes) -> int:
+    buf = np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, np.uint8)
+    return int(datagen().dg_fnv1a64(buf.ctypes.data, len(b)))
+
+
+def digests(data: np.ndarray, offsets: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    out = np.zeros(len(lens), dtype=np.uint64)
+    datagen().dg_digest_batch(data.ctypes.data, np.ascontiguousarray(offsets, np.uint64).ctypes.data,
+                              np.ascontiguousarray(lens, np.uint32).ctypes.data, len(lens),
+                              out.ctypes.data)
+    return out

@@ -1,0 +1,132 @@
+/*
+ * flare_snappy_gpu.h -- C ABI of the MI355X (gfx950) batched Snappy codec.
+ *
+ * This is the drop-in boundary underneath flare's CompressType plugin
+ * surface.  Each entry point replaces one piece of the reference's CPU path
+ * (paths relative to /root/reference):
+ *
+ *   fsg_max_compressed_length      flare/io/snappy/snappy.cc:55-77
+ *                                  (snappy::MaxCompressedLength)
+ *   fsg_get_uncompressed_length    snappy.cc:235-244 (strict,
+ *                                  GetUncompressedLength(const char*,...))
+ *                                  and snappy.cc:692-711 / 870-873 (lenient,
+ *                                  GetUncompressedLength(Source*,...))
+ *   fsg_compress_batch             snappy.cc:875-954 (snappy::Compress(Source*,
+ *                                  Sink*)) as called per message by
+ *                                  flare/rpc/policy/snappy_compress.cc:28-38,51-55
+ *   fsg_decompress_batch           snappy.cc:1537-1563 (snappy::Uncompress(
+ *                                  Source*, Sink*)) as called by
+ *                                  snappy_compress.cc:40-49,57-61; with
+ *                                  FSG_FLAG_VALIDATE_ONLY it is
+ *                                  IsValidCompressed (snappy.cc:1290-1299);
+ *                                  with FSG_FLAG_STRICT_HEADER it is the flat
+ *                                  Uncompress(const char*, size_t, string*)
+ *                                  (snappy.cc:1239-1251).
+ *
+ * Conventions: plain C, no exceptions, no torch types.  All buffers passed
+ * to *_batch functions are DEVICE pointers (hipMalloc'd or device-mapped
+ * pinned host memory); `stream` is a hipStream_t (NULL = default stream).
+ * The calls are asynchronous on `stream`: results are valid after the
+ * stream is synchronised.  Every function is thread-safe; no global state
+ * is mutated after fsg_init.
+ *
+ * Per-message status words (int32):
+ *   FSG_OK              the reference returns true and the output bytes are
+ *                       byte-identical to the reference's.
+ *   FSG_CORRUPT         the reference returns false (bad offset, overrun,
+ *                       premature end, trailing tags, truncated tag).
+ *   FSG_BAD_HEADER      the reference returns false while reading the
+ *                       varint uncompressed-length header.
+ *   FSG_SLOT_TOO_SMALL  caller sizing error: the header's uncompressed length
+ *                       exceeds the output slot (not a reference verdict;
+ *                       size slots with fsg_get_uncompressed_length).
+ * On any status other than FSG_OK the content of the output slot is
+ * unspecified (the reference's partial output on failure depends on the
+ * source fragmentation, snappy.cc:866, and every caller discards it).
+ */
+#ifndef FLARE_SNAPPY_GPU_H_
+#define FLARE_SNAPPY_GPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FSG_OK 0
+#define FSG_CORRUPT 1
+#define FSG_BAD_HEADER 2
+#define FSG_SLOT_TOO_SMALL 3
+
+/* Return codes of the host-side calls. */
+#define FSG_SUCCESS 0
+#define FSG_ERR_INVALID_ARG -1
+#define FSG_ERR_HIP -2
+#define FSG_ERR_NO_DEVICE -3
+
+/* decompress flags */
+#define FSG_FLAG_VALIDATE_ONLY 1u /* IsValidCompressed: no output written   */
+#define FSG_FLAG_STRICT_HEADER 2u /* Parse32WithLimit header (flat API)     */
+
+/* Library version string, e.g. "flare-snappy-gpu 0.1 gfx950". */
+const char *fsg_version(void);
+
+/* Binds the calling host thread to `device` and caches its properties.
+ * Idempotent.  Returns FSG_SUCCESS or a negative error. */
+int fsg_init(int device);
+
+/* Last HIP error text seen by this library on the calling thread. */
+const char *fsg_last_error(void);
+
+/* 32 + n + n/6 (snappy.cc:55-77). */
+size_t fsg_max_compressed_length(size_t n);
+
+/* Host-side header parse.  lenient != 0: ReadUncompressedLength rules
+ * (5th byte's high bits dropped); lenient == 0: Parse32WithLimit rules.
+ * Returns the header byte count (1..5), or 0 if the header is invalid. */
+int fsg_get_uncompressed_length(const void *compressed, size_t n,
+                                uint32_t *ulen, int lenient);
+
+/* Device header pass: for each message writes its (lenient or strict)
+ * uncompressed length into d_ulen (0xFFFFFFFF if the header is invalid).
+ * Lets a caller size output slots without a host round trip per message. */
+int fsg_uncompressed_lengths_batch(const uint8_t *d_in, const uint64_t *d_in_off,
+                                   const uint32_t *d_in_len, uint32_t n_msgs,
+                                   uint32_t *d_ulen, int lenient, void *stream);
+
+/* Workspace needed by fsg_compress_batch / fsg_decompress_batch for a batch
+ * of n_msgs messages whose inputs total total_in_bytes.  May be 0. */
+size_t fsg_compress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_bytes);
+size_t fsg_decompress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_bytes);
+
+/* Batched compress.  Message i is d_in[d_in_off[i] .. +d_in_len[i]); its
+ * compressed stream (varint header + 64 KiB fragments, byte-identical to
+ * snappy::Compress) is written to d_out[d_out_off[i] ..]; each slot must
+ * hold fsg_max_compressed_length(d_in_len[i]) bytes and slots must not
+ * overlap.  d_out_len[i] receives the compressed length, d_status[i] FSG_OK.
+ * max_in_len: an upper bound of every d_in_len[i] (sizes the LDS hash
+ * table; pass 0 for "up to 64 KiB-fragment tables"). */
+int fsg_compress_batch(const uint8_t *d_in, const uint64_t *d_in_off,
+                       const uint32_t *d_in_len, uint32_t n_msgs,
+                       uint32_t max_in_len, uint8_t *d_out,
+                       const uint64_t *d_out_off, uint32_t *d_out_len,
+                       int32_t *d_status, void *d_workspace,
+                       size_t workspace_bytes, void *stream);
+
+/* Batched decompress.  Message i's compressed bytes are
+ * d_in[d_in_off[i] .. +d_in_len[i]); output goes to d_out[d_out_off[i] ..]
+ * with capacity d_out_cap[i] (slots must not overlap).  d_out_len[i]
+ * receives the header's uncompressed length, d_status[i] a FSG_* status.
+ * flags: FSG_FLAG_VALIDATE_ONLY (d_out may be NULL), FSG_FLAG_STRICT_HEADER. */
+int fsg_decompress_batch(const uint8_t *d_in, const uint64_t *d_in_off,
+                         const uint32_t *d_in_len, uint32_t n_msgs,
+                         uint8_t *d_out, const uint64_t *d_out_off,
+                         const uint32_t *d_out_cap, uint32_t *d_out_len,
+                         int32_t *d_status, uint32_t flags, void *d_workspace,
+                         size_t workspace_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLARE_SNAPPY_GPU_H_ */

@@ -1,0 +1,13 @@
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+for p in (REPO / "flare-cpp_amd" / "py", REPO / "oracle", REPO / "tests" / "golden", REPO):
+    if str(p) not in sys.path:
+        sys.path.insert(0, str(p))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")

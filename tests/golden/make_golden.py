@@ -1,0 +1,110 @@
+"""Generate the committed golden vectors from the REFERENCE's own Snappy build.
+
+Run in the dev container (where /root/reference exists and `make -C oracle`
+built oracle/_ref/libsnappy_ref.so):
+
+    python tests/golden/make_golden.py
+
+Every expected output below is produced by the reference code
+(flare/io/snappy/snappy.cc compiled in place), driven through a cord_buf-like
+fragmenting Source (8160-byte fragments, flare/io/cord_buf.h:67) and a
+copying Sink -- the same Source/Sink path policy::SnappyCompress /
+SnappyDecompress take (flare/rpc/policy/snappy_compress.cc:28-61).  The
+reference ships no golden vectors of its own; its test inputs
+(test/rpc/rpc_snappy_compress_test.cc) are reproduced here as data.
+
+Outputs (all data, no code):
+  vectors.json   positive vectors: input spec (or hex) -> compressed hex /
+                 (length, fnv1a64)
+  negative.json  decode vectors: compressed hex -> reference verdict, header
+                 length, strict-header verdict, validator verdict
+  digests_*.npz  per-message (compressed_len, fnv1a64) for the first N
+                 messages of the C2/C3/CM/C5 synthetic batches
+"""
+from __future__ import annotations
+
+import json
+import random
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parents[1]
+sys.path.insert(0, str(REPO / "oracle"))
+sys.path.insert(0, str(REPO / "flare-cpp_amd" / "py"))
+
+from bind import Reference  # noqa: E402
+import fsg  # noqa: E402
+from gen_inputs import build_input, positive_specs, negative_cases  # noqa: E402
+
+
+def main():
+    ref = Reference()
+    vectors = []
+    for spec in positive_specs():
+        data = build_input(spec)
+        comp = ref.compress(data)
+        # fragmentation independence: same bytes at other Peek sizes
+        for frag in (1, 7, 65536, 1 << 30):
+            assert ref.compress(data, frag) == comp, spec
+        ok, out = ref.uncompress(comp, len(data))
+        assert ok and out == data, spec
+        entry = dict(spec)
+        entry["input_len"] = len(data)
+        entry["input_fnv"] = "%016x" % fsg.fnv1a64(data)
+        entry["compressed_len"] = len(comp)
+        entry["compressed_fnv"] = "%016x" % fsg.fnv1a64(comp)
+        if len(comp) <= 2048:
+            entry["compressed_hex"] = comp.hex()
+        vectors.append(entry)
+    (HERE / "vectors.json").write_text(json.dumps(vectors, indent=1) + "\n")
+
+    neg = []
+    for name, comp in negative_cases(ref):
+        ok_src, ulen_src = ref.header_source(comp)
+        ok_strict, ulen_strict = ref.header_strict(comp)
+        cap = ulen_src if ok_src and ulen_src <= (1 << 22) else 0
+        if ok_src and ulen_src > (1 << 22):
+            verdict = None  # too large to materialise; only header verdicts recorded
+            out = b""
+        else:
+            verdict, out = ref.uncompress(comp, cap)
+            for frag in (1, 3, 8160):
+                assert ref.uncompress(comp, cap, frag)[0] == verdict, name
+        neg.append({
+            "name": name,
+            "hex": comp.hex(),
+            "header_ok": ok_src,
+            "ulen": ulen_src if ok_src else 0,
+            "strict_header_ok": ok_strict,
+            "ok": verdict,
+            "valid": ref.is_valid(comp),
+            "output_fnv": "%016x" % fsg.fnv1a64(out) if verdict else None,
+        })
+    (HERE / "negative.json").write_text(json.dumps(neg, indent=1) + "\n")
+
+    # Per-config digests (first N messages of each synthetic batch).
+    cfgs = {
+        "C2": (fsg.KIND_RANDOM, np.full(1024, 4096, np.uint32)),
+        "C3": (fsg.KIND_TEXT, np.full(256, 65536, np.uint32)),
+        "CM": (fsg.KIND_MIXED, fsg.mixed_sizes(4096)),
+        "C5": (fsg.KIND_PROTO, fsg.mixed_sizes(1024)),
+    }
+    for name, (kind, sizes) in cfgs.items():
+        b = fsg.make_batch(kind, sizes)
+        clen = np.zeros(len(b), np.uint32)
+        cfnv = np.zeros(len(b), np.uint64)
+        for i in range(len(b)):
+            c = ref.compress(b.item(i))
+            clen[i] = len(c)
+            cfnv[i] = fsg.fnv1a64(c)
+        np.savez(HERE / f"digests_{name}.npz", input_len=b.lens, input_fnv=fsg.digests(b.data, b.offsets, b.lens),
+                 compressed_len=clen, compressed_fnv=cfnv)
+        print(name, len(b), "bodies, ratio %.3f" % (b.total / max(1, int(clen.sum()))))
+    print(len(vectors), "positive vectors,", len(neg), "negative vectors")
+
+
+if __name__ == "__main__":
+    main()

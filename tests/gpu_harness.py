@@ -1,0 +1,61 @@
+"""Shared GPU-test plumbing: move host batches to the device, run the C ABI,
+bring results back.  torch is used only for device allocations/streams."""
+from __future__ import annotations
+
+import numpy as np
+
+import fsg
+
+
+def dev(a: np.ndarray, device="cuda"):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+
+def empty(n: int, dtype, device="cuda"):
+    import torch
+    return torch.empty(max(n, 1), dtype=dtype, device=device)
+
+
+class GpuCodec:
+    def __init__(self):
+        import torch
+        self.torch = torch
+        self.codec = fsg.SnappyGPU(torch.cuda.current_device())
+
+    def compress(self, batch: fsg.Batch):
+        torch = self.torch
+        n = len(batch)
+        caps = np.array([fsg.max_compressed_length(int(x)) for x in batch.lens], dtype=np.uint64)
+        oo, tot = fsg.slot_offsets(caps)
+        d_in = dev(batch.data)
+        d_io, d_il = dev(batch.offsets), dev(batch.lens)
+        d_out = torch.zeros(tot, dtype=torch.uint8, device="cuda")
+        d_oo = dev(oo)
+        d_ol = empty(n, torch.int32)
+        d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
+        mx = int(batch.lens.max()) if n else 0
+        self.codec.compress(d_in, d_io, d_il, n, mx, d_out, d_oo, d_ol, d_st)
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+        ol = d_ol.cpu().numpy()[:n].view(np.uint32)
+        st = d_st.cpu().numpy()[:n]
+        return [out[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() for i in range(n)], st
+
+    def decompress(self, comps: list[bytes], caps: list[int], flags: int = 0):
+        torch = self.torch
+        b = fsg.Batch.from_list(comps)
+        n = len(b)
+        caps = np.array(caps, dtype=np.uint32)
+        oo, tot = fsg.slot_offsets(caps.astype(np.uint64))
+        d_out = torch.zeros(tot, dtype=torch.uint8, device="cuda")
+        d_ol = empty(n, torch.int32)
+        d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
+        self.codec.decompress(dev(b.data), dev(b.offsets), dev(b.lens), n, d_out, dev(oo), dev(caps),
+                              d_ol, d_st, flags=flags)
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+        ol = d_ol.cpu().numpy()[:n].view(np.uint32)
+        st = d_st.cpu().numpy()[:n]
+        outs = [out[int(oo[i]):int(oo[i]) + int(min(ol[i], caps[i]))].tobytes() for i in range(n)]
+        return outs, ol, st

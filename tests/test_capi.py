@@ -1,0 +1,57 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol
+include/flare_snappy_gpu.h declares, and its host-side helpers agree with the
+oracle (no compute calls are made without a GPU)."""
+import ctypes
+import json
+from pathlib import Path
+
+import pytest
+
+import fsg
+from bind import Oracle
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+def test_header_declares_expected_entry_points():
+    syms = fsg.header_symbols()
+    for s in ("fsg_compress_batch", "fsg_decompress_batch", "fsg_max_compressed_length",
+              "fsg_get_uncompressed_length", "fsg_init"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    lib = fsg.load_gpu_lib()
+    missing = [s for s in fsg.header_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    assert lib.fsg_version().decode().startswith("flare-snappy-gpu")
+
+
+def test_max_compressed_length_matches_oracle():
+    lib = fsg.load_gpu_lib()
+    o = Oracle()
+    for n in (0, 1, 7, 4096, 65536, 1 << 20, (1 << 32) - 1):
+        assert lib.fsg_max_compressed_length(n) == o.max_compressed_length(n) == 32 + n + n // 6
+
+
+@pytest.mark.parametrize("lenient", [1, 0])
+def test_host_header_parse_matches_golden(lenient):
+    lib = fsg.load_gpu_lib()
+    for v in json.loads((GOLDEN / "negative.json").read_text()):
+        b = bytes.fromhex(v["hex"])
+        u = ctypes.c_uint32(0)
+        buf = ctypes.create_string_buffer(b, max(1, len(b)))
+        h = lib.fsg_get_uncompressed_length(buf, len(b), ctypes.byref(u), lenient)
+        expect = v["header_ok"] if lenient else v["strict_header_ok"]
+        assert bool(h) == expect, v["name"]
+        if h and lenient:
+            assert u.value == v["ulen"]
+
+
+def test_invalid_arguments_rejected_without_gpu():
+    lib = fsg.load_gpu_lib()
+    # null device pointers with n > 0 are rejected before any HIP call
+    rc = lib.fsg_compress_batch(None, None, None, 5, 0, None, None, None, None, None, 0, None)
+    assert rc == -1
+    rc = lib.fsg_decompress_batch(None, None, None, 5, None, None, None, None, None, 0, None, 0, None)
+    assert rc == -1
