@@ -5,11 +5,12 @@ ARCH     ?= gfx950
 PKG      := flare-cpp_amd
 LIB      := $(PKG)/lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall
-CSRC     := $(PKG)/csrc/capi.hip $(PKG)/csrc/snappy_decode.hip $(PKG)/csrc/snappy_encode.hip
+CSRC     := $(PKG)/csrc/capi.hip $(PKG)/csrc/snappy_decode.hip $(PKG)/csrc/snappy_decode_v2.hip \
+            $(PKG)/csrc/snappy_encode.hip $(PKG)/csrc/snappy_encode_v2.hip
 CHDRS    := $(PKG)/csrc/snappy_device.h include/flare_snappy_gpu.h
 OBJDIR   := build/obj
 
-all: gpu datagen oracle
+all: gpu host datagen oracle cpptests
 
 gpu: $(LIB)/libflare_snappy_gpu.so
 
@@ -20,6 +21,27 @@ $(OBJDIR)/%.o: $(PKG)/csrc/%.hip $(CHDRS)
 $(LIB)/libflare_snappy_gpu.so: $(patsubst $(PKG)/csrc/%.hip,$(OBJDIR)/%.o,$(CSRC))
 	@mkdir -p $(LIB)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+# Host C++ layer (cord_buf, CompressHandler registry, GPU-backed snappy
+# handler + flat API): host-only code built with g++ against the HIP runtime.
+HOSTCXX   := g++ -std=c++17 -O2 -fPIC -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
+HOST_SRC  := $(wildcard $(PKG)/host/*.cc)
+HOST_HDRS := $(wildcard $(PKG)/host/*.h) include/flare_snappy_gpu.h
+host: $(LIB)/libflare_rpc_snappy.so
+
+$(LIB)/libflare_rpc_snappy.so: $(HOST_SRC) $(HOST_HDRS) $(LIB)/libflare_snappy_gpu.so
+	@mkdir -p $(LIB)
+	$(HOSTCXX) -shared -o $@ $(HOST_SRC) -L$(LIB) -lflare_snappy_gpu -L/opt/rocm/lib -lamdhip64 \
+	  -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,/opt/rocm/lib -pthread
+
+# C++ tests mirroring test/rpc/rpc_snappy_compress_test.cc (run by pytest)
+cpptests: build/test_rpc_snappy_compress
+
+build/test_rpc_snappy_compress: tests/cpp/test_rpc_snappy_compress.cc $(HOST_HDRS) $(LIB)/libflare_rpc_snappy.so
+	@mkdir -p build
+	$(HOSTCXX) -o $@ $< -I$(PKG)/host -L$(LIB) -lflare_rpc_snappy -lflare_snappy_gpu \
+	  -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,$(abspath $(LIB)) -Wl,-rpath,'$$ORIGIN/../$(LIB)' \
+	  -Wl,-rpath,/opt/rocm/lib -pthread
 
 datagen: $(LIB)/libflare_datagen.so
 
@@ -34,4 +56,4 @@ clean:
 	rm -rf build $(LIB)/*.so
 	$(MAKE) -C oracle clean
 
-.PHONY: all gpu datagen oracle clean
+.PHONY: all gpu host cpptests datagen oracle clean

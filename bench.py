@@ -110,8 +110,10 @@ def main():
     d_comp_len = torch.zeros(n, dtype=torch.int32, device=dev)
     d_status = torch.zeros(n, dtype=torch.int32, device=dev)
     max_len = int(batch.lens.max())
+    d_ws = codec.compress_workspace(n, max_len)
     # Compressed inputs come from the GPU encoder (checked against the oracle below).
-    codec.compress(d_raw, d_raw_off, d_raw_len, n, max_len, d_comp, d_comp_off, d_comp_len, d_status)
+    codec.compress(d_raw, d_raw_off, d_raw_len, n, max_len, d_comp, d_comp_off, d_comp_len, d_status,
+                   workspace=d_ws)
     torch.cuda.synchronize()
     comp_len = d_comp_len.cpu().numpy().view(np.uint32).copy()
     comp_total = int(comp_len.astype(np.uint64).sum())
@@ -144,7 +146,7 @@ def main():
     else:
         def step():
             codec.compress(d_raw, d_raw_off, d_raw_len, n, max_len, d_comp, d_comp_off, d_comp_len,
-                           d_status, stream=stream)
+                           d_status, stream=stream, workspace=d_ws)
         algo_bytes = raw_total + comp_total
     gen_s = time.time() - t_gen
 
@@ -192,7 +194,7 @@ def main():
     e2e = None
     if not args.no_e2e and rank == 0:
         e2e = end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp_total, n,
-                         max_len, dev)
+                         max_len, dev, d_ws)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -257,7 +259,8 @@ def load_traffic(workload: str):
     return d if d.get("kernel_src") == kernel_source_hash() else None
 
 
-def end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp_total, n, max_len, dev):
+def end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp_total, n, max_len, dev,
+               d_ws):
     """Pinned host -> HBM -> kernel -> pinned host, one pass (reported in DESIGN.md)."""
     stream = torch.cuda.current_stream()
     if op == "decompress":
@@ -289,7 +292,8 @@ def end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp
         if op == "decompress":
             codec.decompress(d_in, d_off_in, d_len_in, n, d_out, d_off_out, d_cap, d_ol, d_st, stream=stream)
         else:
-            codec.compress(d_in, d_off_in, d_len_in, n, max_len, d_out, d_off_out, d_ol, d_st, stream=stream)
+            codec.compress(d_in, d_off_in, d_len_in, n, max_len, d_out, d_off_out, d_ol, d_st, stream=stream,
+                           workspace=d_ws)
         e[2].record(stream)
         h_out.copy_(d_out[:h_out.numel()], non_blocking=True)
         e[3].record(stream)

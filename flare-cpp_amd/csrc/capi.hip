@@ -1,7 +1,9 @@
 // capi.hip -- extern "C" boundary of libflare_snappy_gpu.so.
 // Declarations and the reference interface each call replaces:
 // include/flare_snappy_gpu.h.
+#include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/flare_snappy_gpu.h"
@@ -12,8 +14,17 @@ hipError_t launch_decode(const u8* in, const u64* in_off, const u32* in_len,
                          u32 n_msgs, u8* out, const u64* out_off,
                          const u32* out_cap, u32* out_len, i32* status,
                          u32 flags, hipStream_t stream);
+hipError_t launch_decode_v2(const u8* in, const u64* in_off, const u32* in_len,
+                            u32 n_msgs, u8* out, const u64* out_off,
+                            const u32* out_cap, u32* out_len, i32* status,
+                            u32 flags, hipStream_t stream);
 hipError_t launch_headers(const u8* in, const u64* in_off, const u32* in_len,
                           u32 n_msgs, u32* ulen, int lenient, hipStream_t stream);
+size_t encode_v2_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out);
+hipError_t launch_encode_v2(const u8* in, const u64* in_off, const u32* in_len,
+                            u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
+                            u32* out_len, i32* status, void* ws, size_t ws_bytes,
+                            hipStream_t stream);
 hipError_t launch_encode(const u8* in, const u64* in_off, const u32* in_len,
                          u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                          u32* out_len, i32* status, hipStream_t stream);
@@ -21,6 +32,15 @@ hipError_t launch_encode(const u8* in, const u64* in_off, const u32* in_len,
 
 namespace {
 thread_local char g_err[256] = "";
+
+int env_int(const char* name) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : 0;
+}
+// Kernel variants (0 = automatic).  Initialised from FSG_DECODE_KERNEL /
+// FSG_ENCODE_KERNEL, changeable with fsg_select_kernels for A/B runs.
+std::atomic<int> g_decode_variant{env_int("FSG_DECODE_KERNEL")};
+std::atomic<int> g_encode_variant{env_int("FSG_ENCODE_KERNEL")};
 
 int record(hipError_t e, const char* where) {
   if (e == hipSuccess) return FSG_SUCCESS;
@@ -34,6 +54,14 @@ extern "C" {
 const char* fsg_version(void) { return "flare-snappy-gpu 0.1 gfx950"; }
 
 const char* fsg_last_error(void) { return g_err; }
+
+int fsg_select_kernels(int decode_variant, int encode_variant) {
+  if (decode_variant < 0 || decode_variant > 2 || encode_variant < 0 || encode_variant > 2)
+    return FSG_ERR_INVALID_ARG;
+  g_decode_variant.store(decode_variant);
+  g_encode_variant.store(encode_variant);
+  return FSG_SUCCESS;
+}
 
 int fsg_init(int device) {
   int n = 0;
@@ -76,7 +104,9 @@ int fsg_uncompressed_lengths_batch(const uint8_t* d_in, const uint64_t* d_in_off
                 "fsg_uncompressed_lengths_batch");
 }
 
-size_t fsg_compress_workspace_bytes(uint32_t, uint64_t) { return 0; }
+size_t fsg_compress_workspace_bytes(uint32_t n_msgs, uint32_t max_in_len) {
+  return fsg::encode_v2_workspace_bytes(n_msgs, max_in_len, nullptr);
+}
 size_t fsg_decompress_workspace_bytes(uint32_t, uint64_t) { return 0; }
 
 int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
@@ -85,11 +115,18 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
                        const uint64_t* d_out_off, uint32_t* d_out_len,
                        int32_t* d_status, void* d_workspace,
                        size_t workspace_bytes, void* stream) {
-  (void)d_workspace;
-  (void)workspace_bytes;
   if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off ||
                  !d_out_len || !d_status))
     return FSG_ERR_INVALID_ARG;
+  // Lane-per-message encoder with global-memory tables when the workspace
+  // allows it; otherwise the wave-per-message LDS-table encoder.
+  const int forced = g_encode_variant.load(std::memory_order_relaxed);
+  const size_t need = fsg::encode_v2_workspace_bytes(n_msgs, max_in_len, nullptr);
+  if (forced != 1 && d_workspace && workspace_bytes >= need)
+    return record(fsg::launch_encode_v2(d_in, d_in_off, d_in_len, n_msgs, max_in_len, d_out,
+                                        d_out_off, d_out_len, d_status, d_workspace,
+                                        workspace_bytes, (hipStream_t)stream),
+                  "fsg_compress_batch");
   return record(fsg::launch_encode(d_in, d_in_off, d_in_len, n_msgs, max_in_len,
                                    d_out, d_out_off, d_out_len, d_status,
                                    (hipStream_t)stream),
@@ -108,9 +145,14 @@ int fsg_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
   if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out_len || !d_status ||
                  (!validate && (!d_out || !d_out_off || !d_out_cap))))
     return FSG_ERR_INVALID_ARG;
-  return record(fsg::launch_decode(d_in, d_in_off, d_in_len, n_msgs, d_out,
-                                   d_out_off, d_out_cap, d_out_len, d_status,
-                                   flags, (hipStream_t)stream),
+  // Kernel choice: the batched-piece decoder (v2) unless validating only
+  // (v1 walks tags without touching output).  FSG_DECODE_KERNEL=1 forces v1.
+  const int forced = g_decode_variant.load(std::memory_order_relaxed);
+  const bool use_v1 = validate || forced == 1;
+  auto launch = use_v1 ? fsg::launch_decode : fsg::launch_decode_v2;
+  return record(launch(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
+                       d_out_cap, d_out_len, d_status, flags,
+                       (hipStream_t)stream),
                 "fsg_decompress_batch");
 }
 

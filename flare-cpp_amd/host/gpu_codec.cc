@@ -1,0 +1,335 @@
+// gpu_codec.cc -- see gpu_codec.h.
+#include "gpu_codec.h"
+
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <mutex>
+
+#include "../../include/flare_snappy_gpu.h"
+
+namespace flare::gpu {
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool reserve(size_t n) {
+    if (n <= cap) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n + n / 4 + 4096;
+    if (hipMalloc(&p, want) != hipSuccess) return false;
+    cap = want;
+    return true;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+struct HostBuf {  // pinned host memory, so hipMemcpyAsync is a true DMA
+  void* p = nullptr;
+  size_t cap = 0;
+  bool reserve(size_t n) {
+    if (n <= cap) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n + n / 4 + 4096;
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) return false;
+    cap = want;
+    return true;
+  }
+  ~HostBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+struct Request {
+  const cord_buf* in;
+  cord_buf* out;
+  bool compress;
+  bool ok = false;
+  bool done = false;
+};
+
+inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+}  // namespace
+
+struct SnappyGpuCodec::Impl {
+  int device = 0;
+  hipStream_t stream = nullptr;
+
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<Request*> queue;
+  bool busy = false;
+
+  DevBuf d_in, d_meta, d_out, d_ws;
+  HostBuf h_in, h_meta, h_out;
+  CodecStats stats;
+
+  // Runs one device batch for `reqs` (all compress or all decompress).
+  void run(const std::vector<Request*>& reqs, bool compress);
+};
+
+SnappyGpuCodec& SnappyGpuCodec::Instance() {
+  static SnappyGpuCodec* inst = new SnappyGpuCodec();  // never destroyed: handlers may run at exit
+  return *inst;
+}
+
+SnappyGpuCodec::SnappyGpuCodec() : impl_(new Impl) {
+  const char* dev = getenv("FLARE_SNAPPY_GPU_DEVICE");
+  impl_->device = dev ? atoi(dev) : 0;
+  if (fsg_init(impl_->device) != FSG_SUCCESS) {
+    err_ = std::string("fsg_init failed: ") + fsg_last_error();
+    return;
+  }
+  if (hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking) != hipSuccess) {
+    err_ = "hipStreamCreate failed";
+    return;
+  }
+  ok_ = true;
+}
+
+SnappyGpuCodec::~SnappyGpuCodec() {
+  if (impl_->stream) (void)hipStreamDestroy(impl_->stream);
+  delete impl_;
+}
+
+CodecStats SnappyGpuCodec::stats() const {
+  std::lock_guard<std::mutex> lk(impl_->mu);
+  return impl_->stats;
+}
+
+void SnappyGpuCodec::Impl::run(const std::vector<Request*>& reqs, bool compress) {
+  const uint32_t n = (uint32_t)reqs.size();
+  if (n == 0) return;
+  if (hipSetDevice(device) != hipSuccess) return;
+  // ---- sizes and layout
+  std::vector<uint32_t> ulen(n, 0);
+  std::vector<uint8_t> skip(n, 0);
+  size_t total_in = 0, total_out = 0;
+  uint32_t max_len = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const size_t len = reqs[i]->in->size();
+    if (len > 0xffffffffu) {  // beyond the format's uint32 lengths
+      skip[i] = 1;
+      continue;
+    }
+    total_in += align16(len);
+    if (compress) {
+      total_out += align16(fsg_max_compressed_length(len));
+      max_len = std::max<uint32_t>(max_len, (uint32_t)len);
+    } else {
+      uint8_t hdr[5];
+      const size_t k = reqs[i]->in->copy_to(hdr, sizeof(hdr));
+      uint32_t u = 0;
+      if (fsg_get_uncompressed_length(hdr, k, &u, /*lenient=*/1) == 0) {
+        skip[i] = 1;  // header unreadable: the reference returns false
+        continue;
+      }
+      // A valid stream expands at most 64/3x (a 3-byte COPY_2 of length 64):
+      // anything larger cannot decode, and the reference returns false.
+      if ((uint64_t)u > 22ull * len + 64) {
+        skip[i] = 1;
+        continue;
+      }
+      ulen[i] = u;
+      total_out += align16(u);
+    }
+  }
+  // metadata: in_off u64, in_len u32, out_off u64, out_cap u32, out_len u32, status i32
+  const size_t meta_bytes = (size_t)n * (8 + 4 + 8 + 4 + 4 + 4);
+  if (!h_in.reserve(total_in + 16) || !h_meta.reserve(meta_bytes) || !h_out.reserve(total_out + 16) ||
+      !d_in.reserve(total_in + 16) || !d_meta.reserve(meta_bytes) || !d_out.reserve(total_out + 16)) {
+    return;  // every request stays !ok
+  }
+  uint8_t* m = h_meta.as<uint8_t>();
+  auto* in_off = reinterpret_cast<uint64_t*>(m);
+  auto* out_off = reinterpret_cast<uint64_t*>(m + 8ull * n);
+  auto* in_len = reinterpret_cast<uint32_t*>(m + 16ull * n);
+  auto* out_cap = reinterpret_cast<uint32_t*>(m + 20ull * n);
+  auto* out_len = reinterpret_cast<uint32_t*>(m + 24ull * n);
+  auto* status = reinterpret_cast<int32_t*>(m + 28ull * n);
+  // ---- gather: cord_buf backing blocks -> pinned staging (cord_buf.cc:1469-1475)
+  uint8_t* hin = h_in.as<uint8_t>();
+  size_t pos_in = 0, pos_out = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    in_off[i] = pos_in;
+    out_off[i] = pos_out;
+    if (skip[i]) {
+      in_len[i] = 0;
+      out_cap[i] = 0;
+      continue;
+    }
+    const cord_buf& in = *reqs[i]->in;
+    size_t w = 0;
+    for (size_t b = 0; b < in.backing_block_num(); ++b) {
+      std::string_view blk = in.backing_block(b);
+      memcpy(hin + pos_in + w, blk.data(), blk.size());
+      w += blk.size();
+    }
+    in_len[i] = (uint32_t)w;
+    pos_in += align16(w);
+    const size_t cap = compress ? fsg_max_compressed_length(w) : ulen[i];
+    out_cap[i] = (uint32_t)cap;
+    pos_out += align16(cap);
+  }
+  // ---- H2D, kernels, D2H on one stream
+  uint8_t* dm = d_meta.as<uint8_t>();
+  if (hipMemcpyAsync(d_in.p, hin, pos_in ? pos_in : 1, hipMemcpyHostToDevice, stream) != hipSuccess ||
+      hipMemcpyAsync(dm, m, 24ull * n, hipMemcpyHostToDevice, stream) != hipSuccess) {  // offsets, lens, caps
+    fprintf(stderr, "[flare-snappy-gpu] H2D copy failed\n");
+    return;
+  }
+  auto* d_in_off = reinterpret_cast<uint64_t*>(dm);
+  auto* d_out_off = reinterpret_cast<uint64_t*>(dm + 8ull * n);
+  auto* d_in_len = reinterpret_cast<uint32_t*>(dm + 16ull * n);
+  auto* d_out_cap = reinterpret_cast<uint32_t*>(dm + 20ull * n);
+  auto* d_out_len = reinterpret_cast<uint32_t*>(dm + 24ull * n);
+  auto* d_status = reinterpret_cast<int32_t*>(dm + 28ull * n);
+  int rc;
+  if (compress) {
+    const size_t ws = fsg_compress_workspace_bytes(n, max_len);
+    void* wsp = d_ws.reserve(ws) ? d_ws.p : nullptr;  // no workspace -> LDS-table kernel
+    rc = fsg_compress_batch(d_in.as<uint8_t>(), d_in_off, d_in_len, n, max_len, d_out.as<uint8_t>(),
+                            d_out_off, d_out_len, d_status, wsp, wsp ? ws : 0, stream);
+  } else {
+    rc = fsg_decompress_batch(d_in.as<uint8_t>(), d_in_off, d_in_len, n, d_out.as<uint8_t>(), d_out_off,
+                              d_out_cap, d_out_len, d_status, 0, nullptr, 0, stream);
+  }
+  if (rc != FSG_SUCCESS) {
+    fprintf(stderr, "[flare-snappy-gpu] batch launch failed: %s\n", fsg_last_error());
+    return;
+  }
+  if (hipMemcpyAsync(m + 24ull * n, d_out_len, 8ull * n, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipMemcpyAsync(h_out.p, d_out.p, pos_out ? pos_out : 1, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+      hipStreamSynchronize(stream) != hipSuccess) {
+    fprintf(stderr, "[flare-snappy-gpu] stream error\n");
+    return;
+  }
+  // ---- scatter: append results to the callers' cord_bufs
+  const uint8_t* hout = h_out.as<uint8_t>();
+  uint64_t bytes_out = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    Request* r = reqs[i];
+    if (skip[i] || status[i] != FSG_OK) {
+      r->ok = false;
+      continue;
+    }
+    r->out->append(hout + out_off[i], out_len[i]);
+    r->ok = true;
+    bytes_out += out_len[i];
+  }
+  std::lock_guard<std::mutex> lk(mu);
+  stats.batches += 1;
+  stats.messages += n;
+  stats.bytes_in += pos_in;
+  stats.bytes_out += bytes_out;
+  stats.max_batch = std::max<uint64_t>(stats.max_batch, n);
+}
+
+namespace {
+// Leader/follower coalescing: whoever finds the runtime idle drains the queue.
+bool submit(SnappyGpuCodec::Impl* impl, Request* r);
+}  // namespace
+
+bool SnappyGpuCodec::Compress(const cord_buf& in, cord_buf* out) {
+  if (!ok_) return false;
+  Request r{&in, out, true};
+  return submit(impl_, &r);
+}
+
+bool SnappyGpuCodec::Uncompress(const cord_buf& in, cord_buf* out) {
+  if (!ok_) return false;
+  Request r{&in, out, false};
+  return submit(impl_, &r);
+}
+
+namespace {
+bool submit(SnappyGpuCodec::Impl* impl, Request* r) {
+  std::unique_lock<std::mutex> lk(impl->mu);
+  impl->queue.push_back(r);
+  while (!r->done) {
+    if (!impl->busy) {
+      impl->busy = true;
+      std::vector<Request*> comp, decomp;
+      for (Request* q : impl->queue) (q->compress ? comp : decomp).push_back(q);
+      impl->queue.clear();
+      lk.unlock();
+      impl->run(comp, true);
+      impl->run(decomp, false);
+      lk.lock();
+      for (Request* q : comp) {
+        if (!q->ok) impl->stats.failures += 1;
+        q->done = true;
+      }
+      for (Request* q : decomp) {
+        if (!q->ok) impl->stats.failures += 1;
+        q->done = true;
+      }
+      impl->busy = false;
+      impl->cv.notify_all();
+    } else {
+      impl->cv.wait(lk);
+    }
+  }
+  return r->ok;
+}
+}  // namespace
+
+static bool run_explicit(SnappyGpuCodec::Impl* impl, bool ok, const std::vector<const cord_buf*>& in,
+                         const std::vector<cord_buf*>& out, std::vector<bool>* res, bool compress) {
+  if (in.size() != out.size()) return false;
+  res->assign(in.size(), false);
+  if (!ok) return false;
+  std::vector<Request> rs(in.size());
+  std::vector<Request*> ps(in.size());
+  for (size_t i = 0; i < in.size(); ++i) {
+    rs[i] = Request{in[i], out[i], compress};
+    ps[i] = &rs[i];
+  }
+  {
+    // serialise with the coalescing path: wait until idle, then run
+    std::unique_lock<std::mutex> lk(impl->mu);
+    impl->cv.wait(lk, [&] { return !impl->busy; });
+    impl->busy = true;
+  }
+  impl->run(ps, compress);
+  {
+    std::lock_guard<std::mutex> lk(impl->mu);
+    impl->busy = false;
+  }
+  impl->cv.notify_all();
+  bool all = true;
+  for (size_t i = 0; i < in.size(); ++i) {
+    (*res)[i] = rs[i].ok;
+    all = all && rs[i].ok;
+  }
+  return all;
+}
+
+bool SnappyGpuCodec::CompressBatch(const std::vector<const cord_buf*>& in,
+                                   const std::vector<cord_buf*>& out, std::vector<bool>* ok) {
+  return run_explicit(impl_, ok_, in, out, ok, true);
+}
+
+bool SnappyGpuCodec::UncompressBatch(const std::vector<const cord_buf*>& in,
+                                     const std::vector<cord_buf*>& out, std::vector<bool>* ok) {
+  return run_explicit(impl_, ok_, in, out, ok, false);
+}
+
+}  // namespace flare::gpu

@@ -28,10 +28,11 @@ _SIGS = {
     "fsg_version": (_c.c_char_p, []),
     "fsg_init": (_c.c_int, [_c.c_int]),
     "fsg_last_error": (_c.c_char_p, []),
+    "fsg_select_kernels": (_c.c_int, [_c.c_int, _c.c_int]),
     "fsg_max_compressed_length": (_sz, [_sz]),
     "fsg_get_uncompressed_length": (_c.c_int, [_vp, _sz, _c.POINTER(_u32), _c.c_int]),
     "fsg_uncompressed_lengths_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _c.c_int, _vp]),
-    "fsg_compress_workspace_bytes": (_sz, [_u32, _u64]),
+    "fsg_compress_workspace_bytes": (_sz, [_u32, _u32]),
     "fsg_decompress_workspace_bytes": (_sz, [_u32, _u64]),
     "fsg_compress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "fsg_decompress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
@@ -72,6 +73,9 @@ class SnappyGPU:
             raise RuntimeError(f"fsg_init({device}) = {rc}: {self.lib.fsg_last_error().decode()}")
         self.device = device
 
+    def select_kernels(self, decode: int = 0, encode: int = 0):
+        self._check(self.lib.fsg_select_kernels(decode, encode), "fsg_select_kernels")
+
     def _check(self, rc: int, what: str):
         if rc != 0:
             raise RuntimeError(f"{what} failed rc={rc}: {self.lib.fsg_last_error().decode()}")
@@ -82,6 +86,12 @@ class SnappyGPU:
             import torch
             return torch.cuda.current_stream().cuda_stream
         return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+    def compress_workspace(self, n, max_in_len, device=None):
+        """Allocate the device workspace fsg_compress_batch wants (torch uint8)."""
+        import torch
+        nbytes = self.lib.fsg_compress_workspace_bytes(n, max_in_len)
+        return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device or f"cuda:{self.device}")
 
     def compress(self, d_in, d_in_off, d_in_len, n, max_in_len, d_out, d_out_off, d_out_len,
                  d_status, stream=None, workspace=None):

@@ -79,6 +79,14 @@ int fsg_init(int device);
 /* Last HIP error text seen by this library on the calling thread. */
 const char *fsg_last_error(void);
 
+/* Kernel variants for A/B measurement and tests: 0 = automatic choice,
+ * 1 = first-generation kernels (decode: one lane per message, tag by tag;
+ * encode: one wave per message with the hash table in LDS), 2 = current
+ * kernels (decode: batched pieces; encode: lane per message, tables in the
+ * workspace).  Every variant produces identical bytes and statuses.
+ * Process-wide; not for use while other threads launch batches. */
+int fsg_select_kernels(int decode_variant, int encode_variant);
+
 /* 32 + n + n/6 (snappy.cc:55-77). */
 size_t fsg_max_compressed_length(size_t n);
 
@@ -95,9 +103,13 @@ int fsg_uncompressed_lengths_batch(const uint8_t *d_in, const uint64_t *d_in_off
                                    const uint32_t *d_in_len, uint32_t n_msgs,
                                    uint32_t *d_ulen, int lenient, void *stream);
 
-/* Workspace needed by fsg_compress_batch / fsg_decompress_batch for a batch
- * of n_msgs messages whose inputs total total_in_bytes.  May be 0. */
-size_t fsg_compress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_bytes);
+/* Device workspace for fsg_compress_batch: per-lane hash tables (one
+ * htsize x u16 table per concurrently encoding lane, htsize per
+ * WorkingMemory::GetHashTable, snappy.cc:247-271) plus a work counter.
+ * max_in_len bounds every message length of the batch (0 = any).  Passing a
+ * smaller or NULL workspace selects the LDS-table wave-per-message encoder. */
+size_t fsg_compress_workspace_bytes(uint32_t n_msgs, uint32_t max_in_len);
+/* Device workspace for fsg_decompress_batch (currently 0). */
 size_t fsg_decompress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_bytes);
 
 /* Batched compress.  Message i is d_in[d_in_off[i] .. +d_in_len[i]); its

@@ -18,8 +18,9 @@ def empty(n: int, dtype, device="cuda"):
 
 
 class GpuCodec:
-    def __init__(self):
+    def __init__(self, use_workspace: bool = True):
         import torch
+        self.use_workspace = use_workspace
         self.torch = torch
         self.codec = fsg.SnappyGPU(torch.cuda.current_device())
 
@@ -35,7 +36,8 @@ class GpuCodec:
         d_ol = empty(n, torch.int32)
         d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
         mx = int(batch.lens.max()) if n else 0
-        self.codec.compress(d_in, d_io, d_il, n, mx, d_out, d_oo, d_ol, d_st)
+        ws = self.codec.compress_workspace(n, mx) if self.use_workspace else None
+        self.codec.compress(d_in, d_io, d_il, n, mx, d_out, d_oo, d_ol, d_st, workspace=ws)
         torch.cuda.synchronize()
         out = d_out.cpu().numpy()
         ol = d_ol.cpu().numpy()[:n].view(np.uint32)

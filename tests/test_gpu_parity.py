@@ -140,6 +140,27 @@ def test_decode_fuzz_against_oracle(gpu, oracle):
             assert s == fsg.FSG_OK and o[:ulen] == ref
 
 
+@pytest.mark.parametrize("variant", [1, 2])
+def test_kernel_variants_agree(gpu, oracle, variant):
+    """Both generations of kernels give the oracle's bytes and statuses."""
+    gpu.codec.select_kernels(variant, variant)
+    try:
+        vecs = json.loads((GOLDEN / "vectors.json").read_text())
+        datas = [build_input(v) for v in vecs if v["input_len"] <= 200000]
+        comps, st = gpu.compress(fsg.Batch.from_list(datas))
+        assert (st == 0).all()
+        assert all(c == oracle.compress(d) for c, d in zip(comps, datas))
+        outs, ol, st = gpu.decompress(comps, [len(d) for d in datas])
+        assert (st == 0).all() and all(o == d for o, d in zip(outs, datas))
+        negs = [v for v in json.loads((GOLDEN / "negative.json").read_text()) if v["ok"] is not None]
+        _, _, st = gpu.decompress([bytes.fromhex(v["hex"]) for v in negs],
+                                  [v["ulen"] if v["header_ok"] else 0 for v in negs])
+        for v, s in zip(negs, st):
+            assert (s == 0) == bool(v["ok"]), v["name"]
+    finally:
+        gpu.codec.select_kernels(0, 0)
+
+
 def test_empty_batch_and_empty_messages(gpu):
     comps, st = gpu.compress(fsg.Batch.from_list([b"", b"", b"x"]))
     assert comps == [b"\x00", b"\x00", b"\x01\x00x"] and (st == 0).all()

@@ -1,0 +1,31 @@
+"""The host C++ drop-in (cord_buf, CompressHandler registry, GPU-backed
+policy::SnappyCompress/SnappyDecompress, flat flare::snappy API, cross-call
+batcher), exercised by tests/cpp/test_rpc_snappy_compress.cc -- the reference's
+rpc_snappy_compress_test.cc cases re-run against the GPU handler."""
+import subprocess
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+BIN = REPO / "build" / "test_rpc_snappy_compress"
+
+
+def _binary():
+    if not BIN.exists():
+        subprocess.run(["make", "-C", str(REPO), "cpptests"], check=True, capture_output=True)
+    return BIN
+
+
+def test_host_layer_cpu_cases():
+    r = subprocess.run([str(_binary()), "--cpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout
+
+
+@pytest.mark.gpu
+def test_host_layer_gpu_cases():
+    r = subprocess.run([str(_binary()), "--gpu"], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout
