@@ -28,6 +28,7 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "flare-cpp_amd" / "py"))
 
 import fsg  # noqa: E402
+import shard  # noqa: E402
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
@@ -65,16 +66,16 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--verify-sample", type=int, default=64)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: every GPU owns a full batch; strong: one batch split by bytes")
     return ap.parse_args()
 
 
-def build_inputs(kind, n, size_spec, first_index):
+def batch_sizes(size_spec, first_index, n):
     if size_spec == "mixed":
-        # shard r of the CM/C5 size stream: regenerate the stream prefix and slice
-        sizes = fsg.mixed_sizes(first_index + n)[first_index:]
-    else:
-        sizes = np.full(n, size_spec, dtype=np.uint32)
-    return fsg.make_batch(kind, sizes, first_index=first_index)
+        # shard of the CM/C5 size stream: regenerate the stream prefix and slice
+        return fsg.mixed_sizes(first_index + n)[first_index:]
+    return np.full(n, size_spec, dtype=np.uint32)
 
 
 def main():
@@ -92,10 +93,14 @@ def main():
     codec = fsg.SnappyGPU(local)
 
     op, kind, n_default, size_spec, desc = WORKLOADS[args.workload]
-    n = args.n_msgs or n_default
-    first = rank * n  # weak scaling: each rank owns messages [rank*n, (rank+1)*n)
+    n_cfg = args.n_msgs or n_default
     t_gen = time.time()
-    batch = build_inputs(kind, n, size_spec, first)
+    if args.scaling == "weak":
+        first, last = shard.weak_range(n_cfg, rank)  # rank owns [rank*n, (rank+1)*n)
+    else:
+        first, last = shard.byte_balanced_ranges(batch_sizes(size_spec, 0, n_cfg), world)[rank]
+    n = last - first
+    batch = fsg.make_batch(kind, batch_sizes(size_spec, first, n), first_index=first)
     raw_total = batch.total
 
     def H(a):
@@ -180,12 +185,8 @@ def main():
 
     t_step = wall / args.steps
     if world > 1:
-        t = torch.tensor([t_step, avg_kernel_s], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_step, avg_kernel_s = float(t[0]), float(t[1])
-        s = torch.tensor([raw_total, comp_total, errors, int(not roundtrip_ok)], dtype=torch.int64, device=dev)
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        raw_all, comp_all, errors, bad = (int(x) for x in s.tolist())
+        t_step, avg_kernel_s, (raw_all, comp_all, errors, bad) = shard.reduce_measurements(
+            dist, dev, t_step, avg_kernel_s, raw_total, comp_total, errors, int(not roundtrip_ok))
         roundtrip_ok = bad == 0
     else:
         raw_all, comp_all = raw_total, comp_total
@@ -213,7 +214,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(t_step * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64-seeded bodies, SURVEY.md §8(d)); compressed by the GPU "
@@ -222,11 +223,12 @@ def main():
                 "workload": desc,
                 "op": op,
                 "messages_per_gpu": n,
-                "global_batch": n * world,
+                "global_batch": n * world if args.scaling == "weak" else n_cfg,
                 "raw_bytes_per_gpu": raw_total,
                 "compressed_bytes_per_gpu": comp_total,
                 "ratio": round(raw_total / max(1, comp_total), 4),
-                "parallelism": f"shard{world} (messages by index, no data-path collective)",
+                "parallelism": f"shard{world} ({args.scaling}: messages by index"
+                               f"{', byte-balanced' if args.scaling == 'strong' else ''}; no data-path collective)",
             },
             "roofline": {
                 "bound": "hbm",
