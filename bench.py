@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--verify-sample", type=int, default=64)
+    ap.add_argument("--decode-lanes", type=int, default=-1,
+                    help="lanes in flight for the persistent decoder (-1 = library default)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: every GPU owns a full batch; strong: one batch split by bytes")
     return ap.parse_args()
@@ -142,11 +144,14 @@ def main():
     d_cap = d_raw_len
     d_comp_len_u = d_comp_len  # int32 view is fine: lengths < 2^31
     stream = torch.cuda.current_stream()
+    d_dws = codec.decompress_workspace(n)
+    if args.decode_lanes >= 0:
+        codec.set_decode_lanes(args.decode_lanes)
 
     if op == "decompress":
         def step():
             codec.decompress(d_comp, d_comp_off, d_comp_len_u, n, d_out, d_raw_off, d_cap, d_out_len,
-                             d_status, stream=stream)
+                             d_status, stream=stream, workspace=d_dws)
         algo_bytes = raw_total + comp_total  # each input byte read once, each output byte written once
     else:
         def step():
@@ -246,6 +251,7 @@ def main():
             "end_to_end": e2e,
             "correct": {"status_errors": errors, "roundtrip_ok": roundtrip_ok, "oracle_sample_ok": sample_ok},
             "kernel_src": kernel_source_hash(),
+            "decode_lanes": args.decode_lanes,
             "setup_s": round(gen_s, 2),
         }
         print(json.dumps(line), flush=True)
@@ -265,6 +271,9 @@ def end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp
                d_ws):
     """Pinned host -> HBM -> kernel -> pinned host, one pass (reported in DESIGN.md)."""
     stream = torch.cuda.current_stream()
+    d_dws = codec.decompress_workspace(n)
+    if args.decode_lanes >= 0:
+        codec.set_decode_lanes(args.decode_lanes)
     if op == "decompress":
         h_in = torch.empty(d_comp.numel(), dtype=torch.uint8, pin_memory=True)
         h_in.copy_(d_comp.cpu())

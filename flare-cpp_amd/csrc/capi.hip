@@ -17,7 +17,7 @@ hipError_t launch_decode(const u8* in, const u64* in_off, const u32* in_len,
 hipError_t launch_decode_v2(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u8* out, const u64* out_off,
                             const u32* out_cap, u32* out_len, i32* status,
-                            u32 flags, hipStream_t stream);
+                            u32 flags, u32* counter, u32 lanes, hipStream_t stream);
 hipError_t launch_headers(const u8* in, const u64* in_off, const u32* in_len,
                           u32 n_msgs, u32* ulen, int lenient, hipStream_t stream);
 size_t encode_v2_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out);
@@ -41,6 +41,10 @@ int env_int(const char* name) {
 // FSG_ENCODE_KERNEL, changeable with fsg_select_kernels for A/B runs.
 std::atomic<int> g_decode_variant{env_int("FSG_DECODE_KERNEL")};
 std::atomic<int> g_encode_variant{env_int("FSG_ENCODE_KERNEL")};
+// Lanes in flight for the persistent decoder (0 = one lane per message).
+// Measured on C3: capping lanes below the message count only removes
+// latency hiding (16384 lanes: 35 ms vs 15 ms with one lane per message).
+std::atomic<unsigned> g_decode_lanes{(unsigned)env_int("FSG_DECODE_LANES")};
 
 int record(hipError_t e, const char* where) {
   if (e == hipSuccess) return FSG_SUCCESS;
@@ -54,6 +58,11 @@ extern "C" {
 const char* fsg_version(void) { return "flare-snappy-gpu 0.1 gfx950"; }
 
 const char* fsg_last_error(void) { return g_err; }
+
+int fsg_set_decode_lanes(uint32_t lanes) {
+  g_decode_lanes.store(lanes);
+  return FSG_SUCCESS;
+}
 
 int fsg_select_kernels(int decode_variant, int encode_variant) {
   if (decode_variant < 0 || decode_variant > 2 || encode_variant < 0 || encode_variant > 2)
@@ -107,7 +116,7 @@ int fsg_uncompressed_lengths_batch(const uint8_t* d_in, const uint64_t* d_in_off
 size_t fsg_compress_workspace_bytes(uint32_t n_msgs, uint32_t max_in_len) {
   return fsg::encode_v2_workspace_bytes(n_msgs, max_in_len, nullptr);
 }
-size_t fsg_decompress_workspace_bytes(uint32_t, uint64_t) { return 0; }
+size_t fsg_decompress_workspace_bytes(uint32_t, uint64_t) { return 256; }
 
 int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
                        const uint32_t* d_in_len, uint32_t n_msgs,
@@ -148,11 +157,18 @@ int fsg_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
   // Kernel choice: the batched-piece decoder (v2) unless validating only
   // (v1 walks tags without touching output).  FSG_DECODE_KERNEL=1 forces v1.
   const int forced = g_decode_variant.load(std::memory_order_relaxed);
-  const bool use_v1 = validate || forced == 1;
-  auto launch = use_v1 ? fsg::launch_decode : fsg::launch_decode_v2;
-  return record(launch(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
-                       d_out_cap, d_out_len, d_status, flags,
-                       (hipStream_t)stream),
+  if (validate || forced == 1)
+    return record(fsg::launch_decode(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
+                                     d_out_cap, d_out_len, d_status, flags,
+                                     (hipStream_t)stream),
+                  "fsg_decompress_batch");
+  // Persistent decode with a bounded number of lanes in flight when the
+  // workspace (a work counter) is provided.
+  fsg::u32* counter = (d_workspace && workspace_bytes >= 4) ? static_cast<fsg::u32*>(d_workspace) : nullptr;
+  return record(fsg::launch_decode_v2(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
+                                      d_out_cap, d_out_len, d_status, flags, counter,
+                                      g_decode_lanes.load(std::memory_order_relaxed),
+                                      (hipStream_t)stream),
                 "fsg_decompress_batch");
 }
 

@@ -29,6 +29,7 @@ _SIGS = {
     "fsg_init": (_c.c_int, [_c.c_int]),
     "fsg_last_error": (_c.c_char_p, []),
     "fsg_select_kernels": (_c.c_int, [_c.c_int, _c.c_int]),
+    "fsg_set_decode_lanes": (_c.c_int, [_u32]),
     "fsg_max_compressed_length": (_sz, [_sz]),
     "fsg_get_uncompressed_length": (_c.c_int, [_vp, _sz, _c.POINTER(_u32), _c.c_int]),
     "fsg_uncompressed_lengths_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _c.c_int, _vp]),
@@ -86,6 +87,14 @@ class SnappyGPU:
             import torch
             return torch.cuda.current_stream().cuda_stream
         return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+    def decompress_workspace(self, n, total_in=0, device=None):
+        import torch
+        nbytes = self.lib.fsg_decompress_workspace_bytes(n, total_in)
+        return torch.zeros(max(nbytes, 1), dtype=torch.uint8, device=device or f"cuda:{self.device}")
+
+    def set_decode_lanes(self, lanes: int):
+        self._check(self.lib.fsg_set_decode_lanes(lanes), "fsg_set_decode_lanes")
 
     def compress_workspace(self, n, max_in_len, device=None):
         """Allocate the device workspace fsg_compress_batch wants (torch uint8)."""

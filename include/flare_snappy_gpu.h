@@ -87,6 +87,10 @@ const char *fsg_last_error(void);
  * Process-wide; not for use while other threads launch batches. */
 int fsg_select_kernels(int decode_variant, int encode_variant);
 
+/* Lanes the persistent decoder keeps in flight (0 = one per message).
+ * Default 16384, or FSG_DECODE_LANES.  Tuning knob; bytes are unaffected. */
+int fsg_set_decode_lanes(uint32_t lanes);
+
 /* 32 + n + n/6 (snappy.cc:55-77). */
 size_t fsg_max_compressed_length(size_t n);
 
@@ -109,7 +113,10 @@ int fsg_uncompressed_lengths_batch(const uint8_t *d_in, const uint64_t *d_in_off
  * max_in_len bounds every message length of the batch (0 = any).  Passing a
  * smaller or NULL workspace selects the LDS-table wave-per-message encoder. */
 size_t fsg_compress_workspace_bytes(uint32_t n_msgs, uint32_t max_in_len);
-/* Device workspace for fsg_decompress_batch (currently 0). */
+/* Device workspace for fsg_decompress_batch: a work counter that lets a
+ * bounded number of lanes (fsg_set_decode_lanes) pull messages, which keeps
+ * each in-flight message's back-reference window resident in L2/MALL.
+ * NULL workspace: one lane per message. */
 size_t fsg_decompress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_bytes);
 
 /* Batched compress.  Message i is d_in[d_in_off[i] .. +d_in_len[i]); its

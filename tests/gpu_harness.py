@@ -53,8 +53,9 @@ class GpuCodec:
         d_out = torch.zeros(tot, dtype=torch.uint8, device="cuda")
         d_ol = empty(n, torch.int32)
         d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
+        ws = self.codec.decompress_workspace(n) if self.use_workspace else None
         self.codec.decompress(dev(b.data), dev(b.offsets), dev(b.lens), n, d_out, dev(oo), dev(caps),
-                              d_ol, d_st, flags=flags)
+                              d_ol, d_st, flags=flags, workspace=ws)
         torch.cuda.synchronize()
         out = d_out.cpu().numpy()
         ol = d_ol.cpu().numpy()[:n].view(np.uint32)

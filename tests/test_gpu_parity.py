@@ -161,6 +161,29 @@ def test_kernel_variants_agree(gpu, oracle, variant):
         gpu.codec.select_kernels(0, 0)
 
 
+@pytest.mark.parametrize("lanes", [0, 64, 1000])
+def test_persistent_decode_lane_counts(gpu, oracle, lanes):
+    """Bounded-lane persistent decode (lanes pull messages from a device
+    counter) gives the same bytes/statuses for any lane count."""
+    gpu.codec.set_decode_lanes(lanes)
+    try:
+        rng = np.random.default_rng(lanes + 1)
+        items = [fsg.make_batch(fsg.KIND_TEXT, [int(rng.integers(0, 70000))], first_index=i).item(0)
+                 for i in range(300)]
+        comps = [oracle.compress(x) for x in items]
+        comps[7] = comps[7][:-3]                       # truncated -> CORRUPT
+        comps[11] = b"\x80"                            # bad header
+        outs, ol, st = gpu.decompress(comps, [len(x) for x in items])
+        for i, (x, c, o, s) in enumerate(zip(items, comps, outs, st)):
+            ok, ulen, ref = oracle.uncompress(c, cap=len(x))
+            assert (s == fsg.FSG_OK) == bool(ok), i
+            if ok:
+                assert o == x
+        assert st[11] == fsg.FSG_BAD_HEADER
+    finally:
+        gpu.codec.set_decode_lanes(16384)
+
+
 def test_empty_batch_and_empty_messages(gpu):
     comps, st = gpu.compress(fsg.Batch.from_list([b"", b"", b"x"]))
     assert comps == [b"\x00", b"\x00", b"\x01\x00x"] and (st == 0).all()
