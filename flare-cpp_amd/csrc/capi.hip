@@ -18,6 +18,10 @@ hipError_t launch_decode_v2(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u8* out, const u64* out_off,
                             const u32* out_cap, u32* out_len, i32* status,
                             u32 flags, u32* counter, u32 lanes, hipStream_t stream);
+hipError_t launch_decode_v3(const u8* in, const u64* in_off, const u32* in_len,
+                            u32 n_msgs, u8* out, const u64* out_off,
+                            const u32* out_cap, u32* out_len, i32* status,
+                            u32 flags, hipStream_t stream);
 hipError_t launch_headers(const u8* in, const u64* in_off, const u32* in_len,
                           u32 n_msgs, u32* ulen, int lenient, hipStream_t stream);
 size_t encode_v2_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out);
@@ -25,6 +29,10 @@ hipError_t launch_encode_v2(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                             u32* out_len, i32* status, void* ws, size_t ws_bytes,
                             hipStream_t stream);
+hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
+                            u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
+                            u32* out_len, i32* status, void* ws, size_t ws_bytes,
+                            u32 slots, u32 entries, hipStream_t stream);
 hipError_t launch_encode(const u8* in, const u64* in_off, const u32* in_len,
                          u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                          u32* out_len, i32* status, hipStream_t stream);
@@ -65,7 +73,7 @@ int fsg_set_decode_lanes(uint32_t lanes) {
 }
 
 int fsg_select_kernels(int decode_variant, int encode_variant) {
-  if (decode_variant < 0 || decode_variant > 2 || encode_variant < 0 || encode_variant > 2)
+  if (decode_variant < 0 || decode_variant > 3 || encode_variant < 0 || encode_variant > 3)
     return FSG_ERR_INVALID_ARG;
   g_decode_variant.store(decode_variant);
   g_encode_variant.store(encode_variant);
@@ -127,11 +135,21 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
   if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off ||
                  !d_out_len || !d_status))
     return FSG_ERR_INVALID_ARG;
-  // Lane-per-message encoder with global-memory tables when the workspace
-  // allows it; otherwise the wave-per-message LDS-table encoder.
+  // Lane-per-message encoders with global-memory tables when the workspace
+  // allows it (v3: batched speculative probes, the default; v2: literal
+  // restatement); otherwise the wave-per-message LDS-table encoder (v1).
   const int forced = g_encode_variant.load(std::memory_order_relaxed);
-  const size_t need = fsg::encode_v2_workspace_bytes(n_msgs, max_in_len, nullptr);
-  if (forced != 1 && d_workspace && workspace_bytes >= need)
+  fsg::u32 slots = 0;
+  const size_t need = fsg::encode_v2_workspace_bytes(n_msgs, max_in_len, &slots);
+  if ((forced == 0 || forced == 3) && d_workspace && workspace_bytes >= need) {
+    const fsg::u32 cap = max_in_len == 0 || max_in_len > fsg::kBlockSize ? fsg::kBlockSize : max_in_len;
+    return record(fsg::launch_encode_v3(d_in, d_in_off, d_in_len, n_msgs, max_in_len, d_out,
+                                        d_out_off, d_out_len, d_status, d_workspace,
+                                        workspace_bytes, slots, fsg::table_size_for(cap),
+                                        (hipStream_t)stream),
+                  "fsg_compress_batch");
+  }
+  if (forced == 2 && d_workspace && workspace_bytes >= need)
     return record(fsg::launch_encode_v2(d_in, d_in_off, d_in_len, n_msgs, max_in_len, d_out,
                                         d_out_off, d_out_len, d_status, d_workspace,
                                         workspace_bytes, (hipStream_t)stream),
@@ -154,15 +172,21 @@ int fsg_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
   if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out_len || !d_status ||
                  (!validate && (!d_out || !d_out_off || !d_out_cap))))
     return FSG_ERR_INVALID_ARG;
-  // Kernel choice: the batched-piece decoder (v2) unless validating only
-  // (v1 walks tags without touching output).  FSG_DECODE_KERNEL=1 forces v1.
+  // Kernel choice: the software-pipelined piece decoder (v3) unless
+  // validating only (v1 walks tags without touching output).
+  // FSG_DECODE_KERNEL=1/2 force v1 / v2 (A/B runs).
   const int forced = g_decode_variant.load(std::memory_order_relaxed);
   if (validate || forced == 1)
     return record(fsg::launch_decode(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
                                      d_out_cap, d_out_len, d_status, flags,
                                      (hipStream_t)stream),
                   "fsg_decompress_batch");
-  // Persistent decode with a bounded number of lanes in flight when the
+  if (forced == 0 || forced == 3)
+    return record(fsg::launch_decode_v3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
+                                        d_out_cap, d_out_len, d_status, flags,
+                                        (hipStream_t)stream),
+                  "fsg_decompress_batch");
+  // v2: persistent decode with a bounded number of lanes in flight when the
   // workspace (a work counter) is provided.
   fsg::u32* counter = (d_workspace && workspace_bytes >= 4) ? static_cast<fsg::u32*>(d_workspace) : nullptr;
   return record(fsg::launch_decode_v2(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,

@@ -1,0 +1,375 @@
+// snappy_encode_v3.hip -- lane-per-message Snappy encode with batched
+// speculative probes, for gfx950.
+//
+// Same unit of work and table placement as encode_lane_kernel (v2): every
+// lane owns a message and a u16 hash table in the workspace, zeroed per
+// fragment (WorkingMemory::GetHashTable, snappy.cc:247-271).  v2 restates
+// internal::CompressFragment (snappy.cc:329-453) literally, paying two
+// dependent global round trips per probe (table entry, then candidate bytes)
+// plus one per 8 bytes of match extension.  v3 keeps the exact greedy parse
+// but resolves it K probes at a time:
+//
+//   * The probe positions of a batch are known in advance: after a copy the
+//     sequence is [ip (after inserting ip-1), ip+1, ip+2, ...], inside a
+//     literal run it is the skip-heuristic sequence p += skip++ >> 5.  Only
+//     the first matching probe ends the batch.
+//   * Round trip 1 loads the K table entries.  A probe that hashes to the
+//     same slot as an earlier probe of the batch (or the ip-1 insertion)
+//     takes that earlier position as its candidate -- exactly what the
+//     sequential table read-then-write would have returned.
+//   * Round trip 2 loads 16 candidate bytes per probe and the input window
+//     for the next batch.  The first probe whose 4 bytes match wins; its match
+//     length is read from the same 16 bytes (99% of C3 matches are <= 16 B);
+//     longer matches extend 16 bytes per load.
+//   * Table writes of the probes up to the winner are then committed in
+//     program order (later writes of a slot win, as in the reference).
+//
+// Input bytes for hashing, for the winner's comparison and for short
+// literals come from an 80-byte per-lane window in LDS ([dword][lane]
+// layout), loaded with the candidates one batch ahead.
+//
+// Output bytes equal snappy::Compress(Source*, Sink*) (snappy.cc:875-954);
+// EmitLiteral / EmitCopy follow snappy.cc:156-232.
+#include "snappy_device.h"
+
+namespace fsg {
+
+namespace {
+
+constexpr int kK = 4;              // probes per batch
+constexpr u32 kWinChunks = 5;      // 80-byte input window
+constexpr u32 kWinDw = kWinChunks * 4;
+
+__device__ u32x4 g_enc_dummy[2];
+
+__device__ __forceinline__ u32 abyte(u32 hi, u32 lo, u32 s) { return __builtin_amdgcn_alignbyte(hi, lo, s); }
+
+// Tag bytes of one EmitCopyLessThan64 (snappy.cc:198-214): packed little
+// endian in the low bytes of the result; *nb = 2 or 3.
+__device__ __forceinline__ u32 copy_tag_lt64(u32 offset, u32 len, u32* nb) {
+  if (len < 12 && offset < 2048) {
+    *nb = 2;
+    return (1u + ((len - 4) << 2) + ((offset >> 8) << 5)) | ((offset & 0xffu) << 8);
+  }
+  *nb = 3;
+  return (2u + ((len - 1) << 2)) | ((offset & 0xffffu) << 8);
+}
+
+// EmitCopy (snappy.cc:216-232).  Stores 4 bytes per tag (the spare bytes are
+// overwritten by later output or lie in the slot's headroom).
+__device__ __forceinline__ u8* emit_copy_v3(u8* op, u32 offset, u32 len) {
+  u32 nb;
+  while (len >= 68) {
+    stu32(op, copy_tag_lt64(offset, 64, &nb));
+    op += nb;
+    len -= 64;
+  }
+  if (len > 64) {
+    stu32(op, copy_tag_lt64(offset, 60, &nb));
+    op += nb;
+    len -= 60;
+  }
+  stu32(op, copy_tag_lt64(offset, len, &nb));
+  return op + nb;
+}
+
+// Literal tag (snappy.cc:156-196); returns the tag length.
+__device__ __forceinline__ u32 literal_tag(u32 len, u64* tag) {
+  const u32 n = len - 1;
+  if (n < 60) { *tag = n << 2; return 1; }
+  const u32 count = n < (1u << 8) ? 1 : n < (1u << 16) ? 2 : n < (1u << 24) ? 3 : 4;
+  *tag = (u64)((59 + count) << 2) | ((u64)n << 8);
+  return 1 + count;
+}
+
+// Literal of `len` bytes copied from global memory (16 bytes at a time; the
+// last store may spill into bytes later output overwrites, or the headroom).
+__device__ __forceinline__ u8* emit_literal_global(u8* op, const u8* lit, u32 len) {
+  u64 tag;
+  const u32 tl = literal_tag(len, &tag);
+  stu64(op, tag);
+  op += tl;
+  u32 k = 0;
+  for (; k + 64 <= len; k += 64) {
+    u32x4 a, b, c, d;
+    __builtin_memcpy(&a, lit + k, 16);
+    __builtin_memcpy(&b, lit + k + 16, 16);
+    __builtin_memcpy(&c, lit + k + 32, 16);
+    __builtin_memcpy(&d, lit + k + 48, 16);
+    __builtin_memcpy(op + k, &a, 16);
+    __builtin_memcpy(op + k + 16, &b, 16);
+    __builtin_memcpy(op + k + 32, &c, 16);
+    __builtin_memcpy(op + k + 48, &d, 16);
+  }
+  for (; k + 16 <= len; k += 16) copy16(op + k, lit + k);
+  for (; k < len; ++k) op[k] = lit[k];
+  return op + len;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void encode_pipe_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off,
+    const u32* __restrict__ in_len, u32 n_msgs, u8* out,
+    const u64* __restrict__ out_off, u32* __restrict__ out_len,
+    i32* __restrict__ status, u16* __restrict__ tables, u32 table_entries,
+    u32* __restrict__ work_counter) {
+  __shared__ u32 win[(kWinDw + 1) * kWave];
+  const u32 lane = threadIdx.x;
+  const u32 slot = blockIdx.x * blockDim.x + lane;
+  u16* table = tables + (u64)slot * table_entries;
+  auto wrd = [&](u32 d) -> u32 { return win[d * kWave + lane]; };
+
+  for (;;) {
+    const u32 m = atomicAdd(work_counter, 1u);
+    if (m >= n_msgs) break;
+    const u8* mb = in + in_off[m];
+    const u32 total = in_len[m];
+    u8* const dst = out + out_off[m];
+    u8* op = dst;
+    {
+      u32 v = total;
+      while (v >= 128) { *op++ = (u8)(v | 128); v >>= 7; }
+      *op++ = (u8)v;
+    }
+    const u32 al = (u32)(reinterpret_cast<uintptr_t>(mb) & 15);
+    const u8* abase = mb - al;
+    const u32 last_chunk = total ? (al + total - 1) >> 4 : 0u;
+
+    for (u32 fpos = 0; fpos < total; fpos += kBlockSize) {
+      const u32 n = min(total - fpos, kBlockSize);
+      const u8* fb = mb + fpos;
+      const u32 ht = table_size_for(n);
+      const int shift = 32 - (31 - __clz((int)ht));
+      {
+        u32x4* t4 = reinterpret_cast<u32x4*>(table);
+        const u32x4 z = {0, 0, 0, 0};
+        for (u32 i = 0; i < ht / 8; ++i) t4[i] = z;
+      }
+      if (n < kInputMarginBytes) {  // snappy.cc:346-347,446-450
+        op = emit_literal_global(op, fb, n);
+        continue;
+      }
+      const u32 lim = n - kInputMarginBytes;
+
+      // ---- input window: chunks [wc, wc + 5) of the message (aligned base)
+      int wbase = 0;  // fragment position of window byte 0
+      auto window_chunks = [&](u32 pos, u32x4 (&g)[kWinChunks]) -> u32 {
+        const u32 c = (al + fpos + pos) >> 4;
+#pragma unroll
+        for (u32 i = 0; i < kWinChunks; ++i) {
+          const u32 k = c + i <= last_chunk ? c + i : last_chunk;
+          __builtin_memcpy(&g[i], abase + 16 * k, 16);
+        }
+        return c;
+      };
+      auto window_store = [&](u32 c, const u32x4 (&g)[kWinChunks]) {
+#pragma unroll
+        for (u32 i = 0; i < kWinChunks; ++i)
+#pragma unroll
+          for (u32 q = 0; q < 4; ++q) win[(4 * i + q) * kWave + lane] = g[i][q];
+        wbase = (int)(16 * c) - (int)(al + fpos);
+      };
+      auto rd32 = [&](u32 pos) -> u32 {
+        const u32 o = (u32)((int)pos - wbase);
+        return abyte(wrd((o >> 2) + 1), wrd(o >> 2), o & 3);
+      };
+      auto in_win = [&](u32 pos, u32 len) -> bool {
+        const int o = (int)pos - wbase;
+        return o >= 0 && o + (int)len <= (int)(16 * kWinChunks);
+      };
+      {
+        u32x4 g0[kWinChunks];
+        const u32 c = window_chunks(0, g0);
+        window_store(c, g0);
+      }
+
+      u32 ip = 1, next_emit = 0, skip = 32;
+      bool post = false;
+      for (;;) {
+        // ---- probe positions of this batch (SK[k]: skip counter at probe k)
+        u32 P[kK], SK[kK];
+        bool live[kK];
+        bool stop = false;  // a scan probe failed its bound: emit_remainder
+        u32 s = post ? ip + 1 : ip, sk = post ? 32u : skip;
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < kK; ++k) {
+          SK[k] = sk;
+          if (k == 0 && post) {
+            P[k] = ip;
+            live[k] = true;
+            continue;
+          }
+          const u32 step = sk >> 5;
+          const bool bound = s + step <= lim;  // next_ip > ip_limit -> remainder
+          stop = stop || (ok && !bound);
+          ok = ok && bound;
+          P[k] = s;
+          live[k] = ok;
+          if (ok) { s += step; ++sk; }
+        }
+        // window: pre-insertion, hash bytes of every live probe
+        const u32 lo_need = post ? ip - 1 : P[0];
+        u32 hi_need = P[0] + 4;
+#pragma unroll
+        for (int k = 0; k < kK; ++k) hi_need = live[k] ? P[k] + 4 : hi_need;
+        if (!in_win(lo_need, hi_need - lo_need)) {
+          u32x4 g0[kWinChunks];
+          const u32 c = window_chunks(lo_need, g0);
+          window_store(c, g0);
+        }
+        // probes past the (reloaded) window wait for the next batch, which
+        // resumes the scan at the first of them
+        int defer_k = -1;
+#pragma unroll
+        for (int k = kK - 1; k >= 0; --k)
+          if (live[k] && !in_win(P[k], 4)) defer_k = k;
+#pragma unroll
+        for (int k = 0; k < kK; ++k) live[k] = live[k] && (defer_k < 0 || k < defer_k);
+        if (defer_k >= 0) {
+          stop = false;
+#pragma unroll
+          for (int k = 0; k < kK; ++k)
+            if (k == defer_k) { s = P[k]; sk = SK[k]; }
+        }
+        u32 X[kK], H[kK];
+#pragma unroll
+        for (int k = 0; k < kK; ++k) {
+          X[k] = live[k] ? rd32(P[k]) : 0u;
+          H[k] = hash_bytes(X[k], shift);
+        }
+        const u32 hpre = post ? hash_bytes(rd32(ip - 1), shift) : 0u;
+        // ---- round trip 1: table entries
+        u32 T[kK];
+#pragma unroll
+        for (int k = 0; k < kK; ++k) T[k] = table[live[k] ? H[k] : 0u];
+        // candidates: the sequential read-then-write order, resolved in registers
+        u32 C[kK];
+#pragma unroll
+        for (int k = 0; k < kK; ++k) {
+          u32 c = T[k];
+          if (post && hpre == H[k]) c = ip - 1;
+#pragma unroll
+          for (int j = 0; j < k; ++j)
+            if (live[j] && H[j] == H[k]) c = P[j];
+          C[k] = c;
+        }
+        // ---- round trip 2: candidate bytes + next window
+        u32x4 CB[kK];
+#pragma unroll
+        for (int k = 0; k < kK; ++k) {
+          const u8* a = live[k] ? fb + C[k] : reinterpret_cast<const u8*>(g_enc_dummy);
+          __builtin_memcpy(&CB[k], a, 16);
+        }
+        u32x4 gn[kWinChunks];
+        const u32 nc = window_chunks(lo_need, gn);
+        // winner
+        int win_k = -1;
+#pragma unroll
+        for (int k = kK - 1; k >= 0; --k)
+          if (live[k] && CB[k][0] == X[k]) win_k = k;
+        // commit table writes (program order)
+        if (post) table[hpre] = (u16)(ip - 1);
+#pragma unroll
+        for (int k = 0; k < kK; ++k)
+          if (live[k] && (win_k < 0 || k <= win_k)) table[H[k]] = (u16)P[k];
+
+        if (win_k >= 0) {
+          u32 p = P[0], cand = C[0];
+          u32x4 cb = CB[0];
+#pragma unroll
+          for (int k = 1; k < kK; ++k)
+            if (win_k == k) { p = P[k]; cand = C[k]; cb = CB[k]; }
+          // literal [next_emit, p)
+          if (p > next_emit) {
+            const u32 len = p - next_emit;
+            if (len <= 16 && in_win(next_emit, 20)) {
+              u64 tag;
+              const u32 tl = literal_tag(len, &tag);
+              *op = (u8)tag;
+              const u32 o = (u32)((int)next_emit - wbase);
+              u32x4 v;
+#pragma unroll
+              for (u32 q = 0; q < 4; ++q) v[q] = abyte(wrd((o >> 2) + q + 1), wrd((o >> 2) + q), o & 3);
+              __builtin_memcpy(op + tl, &v, 16);
+              op += tl + len;
+            } else {
+              op = emit_literal_global(op, fb + next_emit, len);
+            }
+          }
+          // match length: FindMatchLength(cand + 4, p + 4, fragment end)
+          u32 mlen;
+          {
+            u32x4 pb;
+            if (in_win(p, 20)) {
+              const u32 o = (u32)((int)p - wbase);
+#pragma unroll
+              for (u32 q = 0; q < 4; ++q) pb[q] = abyte(wrd((o >> 2) + q + 1), wrd((o >> 2) + q), o & 3);
+            } else if (fpos + p + 16 <= total) {
+              __builtin_memcpy(&pb, fb + p, 16);
+            } else {  // last bytes of the message: load [p-1, p+15) and shift
+              u32x4 t;
+              __builtin_memcpy(&t, fb + p - 1, 16);
+              pb[0] = abyte(t[1], t[0], 1);
+              pb[1] = abyte(t[2], t[1], 1);
+              pb[2] = abyte(t[3], t[2], 1);
+              pb[3] = t[3] >> 8;  // byte p+15 is past the message: clamped below
+            }
+            const u64 x0 = ((u64)(pb[1] ^ cb[1]) << 32) | (pb[0] ^ cb[0]);
+            const u64 x1 = ((u64)(pb[3] ^ cb[3]) << 32) | (pb[2] ^ cb[2]);
+            mlen = x0 ? (u32)(__builtin_ctzll(x0) >> 3) : x1 ? 8 + (u32)(__builtin_ctzll(x1) >> 3) : 16u;
+            if (mlen == 16) {
+              while (p + mlen + 16 <= n) {
+                u32x4 a, b;
+                __builtin_memcpy(&a, fb + cand + mlen, 16);
+                __builtin_memcpy(&b, fb + p + mlen, 16);
+                const u64 y0 = ((u64)(a[1] ^ b[1]) << 32) | (a[0] ^ b[0]);
+                const u64 y1 = ((u64)(a[3] ^ b[3]) << 32) | (a[2] ^ b[2]);
+                if (y0 | y1) {
+                  mlen += y0 ? (u32)(__builtin_ctzll(y0) >> 3) : 8 + (u32)(__builtin_ctzll(y1) >> 3);
+                  goto matched;
+                }
+                mlen += 16;
+              }
+              while (p + mlen < n && fb[cand + mlen] == fb[p + mlen]) ++mlen;
+            }
+          matched:
+            mlen = min(mlen, n - p);
+          }
+          op = emit_copy_v3(op, p - cand, mlen);
+          ip = p + mlen;
+          next_emit = ip;
+          post = true;
+          window_store(nc, gn);
+          if (ip >= lim) break;  // emit_remainder
+        } else {
+          window_store(nc, gn);
+          if (stop) break;       // emit_remainder
+          ip = s;
+          skip = sk;
+          post = false;
+        }
+      }
+      if (next_emit < n) op = emit_literal_global(op, fb + next_emit, n - next_emit);
+    }
+    out_len[m] = (u32)(op - dst);
+    status[m] = kOk;
+  }
+}
+
+hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
+                            u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
+                            u32* out_len, i32* status, void* ws, size_t ws_bytes,
+                            u32 slots, u32 entries, hipStream_t stream) {
+  if (n_msgs == 0) return hipSuccess;
+  u32* counter = reinterpret_cast<u32*>(ws);
+  u16* tables = reinterpret_cast<u16*>(reinterpret_cast<u8*>(ws) + 256);
+  hipError_t e = hipMemsetAsync(counter, 0, 256, stream);
+  if (e != hipSuccess) return e;
+  encode_pipe_kernel<<<slots / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off,
+                                                    out_len, status, tables, entries, counter);
+  return hipGetLastError();
+}
+
+}  // namespace fsg

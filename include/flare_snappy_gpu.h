@@ -81,14 +81,18 @@ const char *fsg_last_error(void);
 
 /* Kernel variants for A/B measurement and tests: 0 = automatic choice,
  * 1 = first-generation kernels (decode: one lane per message, tag by tag;
- * encode: one wave per message with the hash table in LDS), 2 = current
- * kernels (decode: batched pieces; encode: lane per message, tables in the
- * workspace).  Every variant produces identical bytes and statuses.
+ * encode: one wave per message with the hash table in LDS), 2 = second
+ * generation (decode: batched pieces, optional persistent lanes; encode: lane
+ * per message, tables in the workspace), 3 = third generation, the default
+ * (decode: software-pipelined batched pieces; encode: lane per message with
+ * batched speculative probes).  Every variant produces identical bytes and
+ * statuses.
  * Process-wide; not for use while other threads launch batches. */
 int fsg_select_kernels(int decode_variant, int encode_variant);
 
-/* Lanes the persistent decoder keeps in flight (0 = one per message).
- * Default 16384, or FSG_DECODE_LANES.  Tuning knob; bytes are unaffected. */
+/* Lanes the persistent decoder (decode variant 2) keeps in flight
+ * (0 = one per message, the default; or FSG_DECODE_LANES).  Tuning knob;
+ * bytes are unaffected. */
 int fsg_set_decode_lanes(uint32_t lanes);
 
 /* 32 + n + n/6 (snappy.cc:55-77). */

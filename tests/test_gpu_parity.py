@@ -140,9 +140,9 @@ def test_decode_fuzz_against_oracle(gpu, oracle):
             assert s == fsg.FSG_OK and o[:ulen] == ref
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_kernel_variants_agree(gpu, oracle, variant):
-    """Both generations of kernels give the oracle's bytes and statuses."""
+    """Every generation of kernels gives the oracle's bytes and statuses."""
     gpu.codec.select_kernels(variant, variant)
     try:
         vecs = json.loads((GOLDEN / "vectors.json").read_text())
@@ -165,6 +165,7 @@ def test_kernel_variants_agree(gpu, oracle, variant):
 def test_persistent_decode_lane_counts(gpu, oracle, lanes):
     """Bounded-lane persistent decode (lanes pull messages from a device
     counter) gives the same bytes/statuses for any lane count."""
+    gpu.codec.select_kernels(2, 0)
     gpu.codec.set_decode_lanes(lanes)
     try:
         rng = np.random.default_rng(lanes + 1)
@@ -181,7 +182,8 @@ def test_persistent_decode_lane_counts(gpu, oracle, lanes):
                 assert o == x
         assert st[11] == fsg.FSG_BAD_HEADER
     finally:
-        gpu.codec.set_decode_lanes(16384)
+        gpu.codec.set_decode_lanes(0)
+        gpu.codec.select_kernels(0, 0)
 
 
 def test_empty_batch_and_empty_messages(gpu):
@@ -189,3 +191,74 @@ def test_empty_batch_and_empty_messages(gpu):
     assert comps == [b"\x00", b"\x00", b"\x01\x00x"] and (st == 0).all()
     outs, ol, st = gpu.decompress([b"\x00"], [0])
     assert st[0] == 0 and ol[0] == 0
+
+
+def _lit(b: bytes) -> bytes:
+    n = len(b) - 1
+    if n < 60:
+        return bytes([n << 2]) + b
+    k = (n.bit_length() + 7) // 8
+    return bytes([(59 + k) << 2]) + n.to_bytes(k, "little") + b
+
+
+def _copy(off: int, ln: int, wide: bool = False) -> bytes:
+    if wide or off > 0xFFFF:                             # COPY_4
+        return bytes([((ln - 1) << 2) | 3]) + off.to_bytes(4, "little")
+    if 4 <= ln <= 11 and off < 2048:                     # COPY_1
+        return bytes([((off >> 8) << 5) | ((ln - 4) << 2) | 1, off & 0xFF])
+    return bytes([((ln - 1) << 2) | 2]) + off.to_bytes(2, "little")  # COPY_2
+
+
+def _synthetic_stream(rng, target):
+    """A valid-by-construction tag stream stressing what the encoder rarely
+    emits: offsets 1..15 (pattern copies) at every length 1..64, COPY_4,
+    long literals (which jump the decoder's input ring), back-to-back short
+    copies, and output ends at every alignment."""
+    body, out = [], bytearray()
+    first = bytes(rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8))
+    body.append(_lit(first)); out += first
+    while len(out) < target:
+        r = rng.random()
+        if r < 0.45:
+            off = int(rng.integers(1, min(16, len(out)) + 1))
+        elif r < 0.75:
+            off = int(rng.integers(1, min(300, len(out)) + 1))
+        elif r < 0.85:
+            off = int(rng.integers(1, len(out) + 1))
+        else:
+            n = int(rng.integers(1, 3000 if rng.random() < 0.1 else 30))
+            lit = bytes(rng.integers(0, 256, n, dtype=np.uint8))
+            body.append(_lit(lit)); out += lit
+            continue
+        ln = int(rng.integers(1, 65))
+        body.append(_copy(off, ln, wide=rng.random() < 0.05))
+        for _ in range(ln):
+            out.append(out[-off])
+    hdr = bytearray()
+    n = len(out)
+    while n >= 0x80:
+        hdr.append((n & 0x7F) | 0x80); n >>= 7
+    hdr.append(n)
+    return bytes(hdr) + b"".join(body), bytes(out)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_pattern_copies_and_ring_jumps(gpu, oracle, variant):
+    """Hand-built streams: every small offset/length combination, COPY_4 and
+    long literals, at output ends of every alignment; decoded bytes equal the
+    oracle's (and the construction's)."""
+    gpu.codec.select_kernels(variant, 0)
+    try:
+        rng = np.random.default_rng(2024 + variant)
+        comps, raws = [], []
+        for i in range(600):
+            target = int(rng.integers(1, 9000)) if i % 5 else int(rng.integers(20000, 70000))
+            c, raw = _synthetic_stream(rng, target)
+            comps.append(c); raws.append(raw)
+        outs, ol, st = gpu.decompress(comps, [len(r) for r in raws])
+        for i, (c, raw, o, s) in enumerate(zip(comps, raws, outs, st)):
+            ok, ulen, ref = oracle.uncompress(c, cap=len(raw))
+            assert ok and ref == raw, i
+            assert s == fsg.FSG_OK and o == raw, i
+    finally:
+        gpu.codec.select_kernels(0, 0)
