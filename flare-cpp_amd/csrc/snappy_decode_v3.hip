@@ -34,7 +34,14 @@ namespace fsg {
 
 namespace {
 
-constexpr int kP3 = 16;        // pieces per batch
+#ifndef FSG_V3_PIECES
+#define FSG_V3_PIECES 16
+#endif
+#ifndef FSG_V3_LOOKBACK
+#define FSG_V3_LOOKBACK 8
+#endif
+constexpr int kP3 = FSG_V3_PIECES;      // pieces per batch
+constexpr int kLook = FSG_V3_LOOKBACK;  // earlier pieces searched to re-source a hazard
 constexpr u32 kRingChunks = 16;  // 16-byte chunks per lane ring (256 B)
 constexpr u32 kRingDwords = kRingChunks * 4;
 constexpr u32 kAhead = 4;        // chunks fetched per iteration
@@ -244,7 +251,7 @@ __global__ __launch_bounds__(64) void decode_pipe_kernel(
     }
 
     // ---------- B: parse this batch
-    u32 rx[kP3], rm[kP3];
+    u32 rx[kP3], rm[kP3], pdst[kP3];
     const u32 batch_start = op;
     bool closed = status >= 0;
 #pragma unroll
@@ -294,16 +301,36 @@ __global__ __launch_bounds__(64) void decode_pipe_kernel(
       // ---- one piece of the current tag
       const u32 n = rem < pstep ? rem : pstep;
       const bool have = !closed && rem > 0;
-      const bool hazard = have && kind == kKindCopy && src + n > batch_start;
+      // A copy whose source is output still pending in this batch is
+      // re-sourced to where those bytes come from -- the literal's input
+      // bytes or the (already final) source of an earlier copy piece -- if
+      // one of the last kLook pieces covers it; otherwise the batch closes.
+      const bool pend = have && kind == kKindCopy && src + n > batch_start;
+      u32 fdst = 0, fm = 0, fx = 0;
+#pragma unroll
+      for (int k = (j > kLook ? j - kLook : 0); k < j; ++k) {
+        const bool cv = (rm[k] != 0) & (pdst[k] <= src);
+        fdst = cv ? pdst[k] : fdst;
+        fm = cv ? rm[k] : fm;
+        fx = cv ? rx[k] : fx;
+      }
+      const u32 fkind = m_kind(fm);
+      const bool fwd = pend & (fm != 0) & (src >= batch_start) & (src + n <= fdst + m_cnt(fm)) &
+                       (fkind != kKindPat);
+      const bool hazard = pend & !fwd;
       closed = closed || hazard;
       const bool emit = have && !hazard;
-      const bool lit = kind == kKindLit;
+      const u32 fsrc = fx + m_shf(fm) + (src - fdst);
+      const u32 ekind = fwd ? fkind : kind;
+      const u32 esrc = fwd ? fsrc : src;
+      const bool lit = ekind == kKindLit;
       const u32 rlen = lit ? n_in : expected;
       const int lo_off = -(int)(lit ? ibal : obal);
       const int tail = (int)rlen - 16;
-      const int a_off = (src + 16 <= rlen) ? (int)src : (tail > lo_off ? tail : lo_off);
+      const int a_off = (esrc + 16 <= rlen) ? (int)esrc : (tail > lo_off ? tail : lo_off);
       rx[j] = (u32)a_off;
-      rm[j] = emit ? (n | (kind << 5) | ((u32)((int)src - a_off) << 7) |
+      pdst[j] = op;
+      rm[j] = emit ? (n | (ekind << 5) | ((u32)((int)esrc - a_off) << 7) |
                       ((op + 16 > expected ? 1u : 0u) << 11) | (poff << 12))
                    : 0u;
       src += (emit && kind != kKindPat) ? n : 0u;
