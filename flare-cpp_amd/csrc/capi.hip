@@ -143,6 +143,10 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
   const size_t need = fsg::encode_v2_workspace_bytes(n_msgs, max_in_len, &slots);
   if ((forced == 0 || forced == 3) && d_workspace && workspace_bytes >= need) {
     const fsg::u32 cap = max_in_len == 0 || max_in_len > fsg::kBlockSize ? fsg::kBlockSize : max_in_len;
+    // Lanes in flight (tuning knob): fewer lanes keep their tables and
+    // recent input cache-resident; each lane then encodes more messages.
+    static const unsigned lanes_cap = (unsigned)env_int("FSG_ENCODE_LANES");
+    if (lanes_cap && lanes_cap < slots) slots = (lanes_cap + 63) / 64 * 64;
     return record(fsg::launch_encode_v3(d_in, d_in_off, d_in_len, n_msgs, max_in_len, d_out,
                                         d_out_off, d_out_len, d_status, d_workspace,
                                         workspace_bytes, slots, fsg::table_size_for(cap),

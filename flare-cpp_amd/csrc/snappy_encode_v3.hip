@@ -36,7 +36,10 @@ namespace fsg {
 
 namespace {
 
-constexpr int kK = 4;              // probes per batch
+#ifndef FSG_V3_PROBES
+#define FSG_V3_PROBES 2
+#endif
+constexpr int kK = FSG_V3_PROBES;  // probes per batch
 constexpr u32 kWinChunks = 5;      // 80-byte input window
 constexpr u32 kWinDw = kWinChunks * 4;
 
