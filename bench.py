@@ -145,8 +145,6 @@ def main():
     d_comp_len_u = d_comp_len  # int32 view is fine: lengths < 2^31
     stream = torch.cuda.current_stream()
     d_dws = codec.decompress_workspace(n)
-    if args.decode_lanes >= 0:
-        codec.set_decode_lanes(args.decode_lanes)
 
     if op == "decompress":
         def step():
@@ -272,8 +270,6 @@ def end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp
     """Pinned host -> HBM -> kernel -> pinned host, one pass (reported in DESIGN.md)."""
     stream = torch.cuda.current_stream()
     d_dws = codec.decompress_workspace(n)
-    if args.decode_lanes >= 0:
-        codec.set_decode_lanes(args.decode_lanes)
     if op == "decompress":
         h_in = torch.empty(d_comp.numel(), dtype=torch.uint8, pin_memory=True)
         h_in.copy_(d_comp.cpu())

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Profile recipe run on the GPU box (gpurun): bench lines, rocprofv3 kernel
+# trace/stats and the PMC traffic passes for the default workload and for the
+# C2 calibration case.  Each GPU step is time-limited; the chain stops at the
+# first failure.
+set -e
+export TMPDIR=/tmp
+O=gpurun_out/prof
+mkdir -p $O
+B="python bench.py"
+timeout -k 10 300 $B > $O/bench_c3d.json 2> $O/bench_c3d.err
+timeout -k 10 300 $B --workload c3-compress --steps 3 --warmup 1 > $O/bench_c3c.json 2> $O/bench_c3c.err
+timeout -k 10 300 $B --workload c2-decompress --steps 20 --warmup 3 > $O/bench_c2d.json 2> $O/bench_c2d.err
+timeout -k 10 300 $B --workload cm-decompress --steps 5 --warmup 1 > $O/bench_cmd.json 2> $O/bench_cmd.err
+timeout -k 10 300 $B --workload c5-compress --steps 3 --warmup 1 > $O/bench_c5c.json 2> $O/bench_c5c.err
+cd $O
+Q="--steps 3 --warmup 1 --no-e2e --no-cpu-baseline --verify-sample 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d kt -o kt -- python ../../bench.py $Q > kt.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d f3 -o f3 -- python ../../bench.py $Q > f3.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d w3 -o w3 -- python ../../bench.py $Q > w3.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d f2 -o f2 -- python ../../bench.py --workload c2-decompress $Q > f2.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d w2 -o w2 -- python ../../bench.py --workload c2-decompress $Q > w2.log 2>&1
+echo done
