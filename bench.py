@@ -68,6 +68,10 @@ def parse():
     ap.add_argument("--verify-sample", type=int, default=64)
     ap.add_argument("--decode-lanes", type=int, default=-1,
                     help="lanes in flight for the persistent decoder (-1 = library default)")
+    ap.add_argument("--decode-kernel", type=int, default=0,
+                    help="decoder variant (0 = library default, 1-4 = force; A/B runs)")
+    ap.add_argument("--encode-kernel", type=int, default=0,
+                    help="encoder variant (0 = library default, 1-3 = force; A/B runs)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: every GPU owns a full batch; strong: one batch split by bytes")
     return ap.parse_args()
@@ -93,6 +97,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     codec = fsg.SnappyGPU(local)
+    codec.select_kernels(args.decode_kernel, args.encode_kernel)
 
     op, kind, n_default, size_spec, desc = WORKLOADS[args.workload]
     n_cfg = args.n_msgs or n_default
@@ -144,7 +149,7 @@ def main():
     d_cap = d_raw_len
     d_comp_len_u = d_comp_len  # int32 view is fine: lengths < 2^31
     stream = torch.cuda.current_stream()
-    d_dws = codec.decompress_workspace(n)
+    d_dws = codec.decompress_workspace(n, c_tot)
 
     if op == "decompress":
         def step():
@@ -250,6 +255,7 @@ def main():
             "correct": {"status_errors": errors, "roundtrip_ok": roundtrip_ok, "oracle_sample_ok": sample_ok},
             "kernel_src": kernel_source_hash(),
             "decode_lanes": args.decode_lanes,
+            "kernels": {"decode": args.decode_kernel, "encode": args.encode_kernel},
             "setup_s": round(gen_s, 2),
         }
         print(json.dumps(line), flush=True)
@@ -269,7 +275,7 @@ def end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp
                d_ws):
     """Pinned host -> HBM -> kernel -> pinned host, one pass (reported in DESIGN.md)."""
     stream = torch.cuda.current_stream()
-    d_dws = codec.decompress_workspace(n)
+    d_dws = codec.decompress_workspace(n, d_comp.numel())
     if op == "decompress":
         h_in = torch.empty(d_comp.numel(), dtype=torch.uint8, pin_memory=True)
         h_in.copy_(d_comp.cpu())
@@ -297,7 +303,8 @@ def end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp
         d_in.copy_(h_in, non_blocking=True)
         e[1].record(stream)
         if op == "decompress":
-            codec.decompress(d_in, d_off_in, d_len_in, n, d_out, d_off_out, d_cap, d_ol, d_st, stream=stream)
+            codec.decompress(d_in, d_off_in, d_len_in, n, d_out, d_off_out, d_cap, d_ol, d_st, stream=stream,
+                             workspace=d_dws)
         else:
             codec.compress(d_in, d_off_in, d_len_in, n, max_len, d_out, d_off_out, d_ol, d_st, stream=stream,
                            workspace=d_ws)

@@ -22,6 +22,11 @@ hipError_t launch_decode_v3(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u8* out, const u64* out_off,
                             const u32* out_cap, u32* out_len, i32* status,
                             u32 flags, hipStream_t stream);
+size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes);
+hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
+                            u32 n_msgs, u8* out, const u64* out_off,
+                            const u32* out_cap, u32* out_len, i32* status,
+                            u32 flags, void* ws, size_t ws_bytes, hipStream_t stream);
 hipError_t launch_headers(const u8* in, const u64* in_off, const u32* in_len,
                           u32 n_msgs, u32* ulen, int lenient, hipStream_t stream);
 size_t encode_v2_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out);
@@ -73,7 +78,7 @@ int fsg_set_decode_lanes(uint32_t lanes) {
 }
 
 int fsg_select_kernels(int decode_variant, int encode_variant) {
-  if (decode_variant < 0 || decode_variant > 3 || encode_variant < 0 || encode_variant > 3)
+  if (decode_variant < 0 || decode_variant > 4 || encode_variant < 0 || encode_variant > 3)
     return FSG_ERR_INVALID_ARG;
   g_decode_variant.store(decode_variant);
   g_encode_variant.store(encode_variant);
@@ -124,7 +129,10 @@ int fsg_uncompressed_lengths_batch(const uint8_t* d_in, const uint64_t* d_in_off
 size_t fsg_compress_workspace_bytes(uint32_t n_msgs, uint32_t max_in_len) {
   return fsg::encode_v2_workspace_bytes(n_msgs, max_in_len, nullptr);
 }
-size_t fsg_decompress_workspace_bytes(uint32_t, uint64_t) { return 256; }
+size_t fsg_decompress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_bytes) {
+  // total_in_bytes = 0: no size known, only the single-pass decoders run.
+  return total_in_bytes ? fsg::decode_v4_workspace_bytes(n_msgs, total_in_bytes) : 256;
+}
 
 int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
                        const uint32_t* d_in_len, uint32_t n_msgs,
@@ -170,22 +178,34 @@ int fsg_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
                          const uint32_t* d_out_cap, uint32_t* d_out_len,
                          int32_t* d_status, uint32_t flags, void* d_workspace,
                          size_t workspace_bytes, void* stream) {
-  (void)d_workspace;
-  (void)workspace_bytes;
   const bool validate = flags & FSG_FLAG_VALIDATE_ONLY;
   if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out_len || !d_status ||
                  (!validate && (!d_out || !d_out_off || !d_out_cap))))
     return FSG_ERR_INVALID_ARG;
-  // Kernel choice: the software-pipelined piece decoder (v3) unless
-  // validating only (v1 walks tags without touching output).
-  // FSG_DECODE_KERNEL=1/2 force v1 / v2 (A/B runs).
+  // Kernel choice: the two-pass decoder (v4: lane-per-message index pass +
+  // wave-per-message execution) when the workspace holds its tag bitmap;
+  // otherwise the software-pipelined lane-per-message decoder (v3); v1 walks
+  // tags without touching output for validate-only.  FSG_DECODE_KERNEL or
+  // fsg_select_kernels force a variant (A/B runs).
   const int forced = g_decode_variant.load(std::memory_order_relaxed);
   if (validate || forced == 1)
     return record(fsg::launch_decode(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
                                      d_out_cap, d_out_len, d_status, flags,
                                      (hipStream_t)stream),
                   "fsg_decompress_batch");
-  if (forced == 0 || forced == 3)
+  const bool v4_fits = d_workspace && workspace_bytes >= fsg::decode_v4_workspace_bytes(n_msgs, 0);
+  if (forced == 4 && v4_fits) {
+    hipError_t e = fsg::launch_decode_v4(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
+                                         d_out_cap, d_out_len, d_status, flags, d_workspace,
+                                         workspace_bytes, (hipStream_t)stream);
+    // messages whose bitmap did not fit the workspace (status kNeedFallback)
+    if (e == hipSuccess)
+      e = fsg::launch_decode_v3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
+                                d_out_len, d_status, flags | fsg::kFlagFallbackOnly,
+                                (hipStream_t)stream);
+    return record(e, "fsg_decompress_batch");
+  }
+  if (forced == 0 || forced == 3 || forced == 4)
     return record(fsg::launch_decode_v3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
                                         d_out_cap, d_out_len, d_status, flags,
                                         (hipStream_t)stream),

@@ -28,7 +28,7 @@
 // Reference checks and statuses are exactly those of decode_lane_kernel
 // (DecompressAllTags snappy.cc:716-787, writer checks :1141-1481,
 // result :858-868).
-#include "snappy_device.h"
+#include "snappy_pieces.h"
 
 namespace fsg {
 
@@ -56,90 +56,6 @@ __device__ __forceinline__ u32 m_off(u32 m) { return (m >> 12) & 15u; }
 
 __device__ u32x4 g_dummy16[1];  // target of the loads of empty pieces
 
-__device__ __forceinline__ u32 alignbyte3(u32 hi, u32 lo, u32 s) {
-  return __builtin_amdgcn_alignbyte(hi, lo, s);
-}
-
-__device__ __forceinline__ u32 mux8v3(const u32 (&w)[8], u32 d) {
-  u32 a0 = (d & 1) ? w[1] : w[0];
-  u32 a1 = (d & 1) ? w[3] : w[2];
-  u32 a2 = (d & 1) ? w[5] : w[4];
-  u32 a3 = (d & 1) ? w[7] : w[6];
-  u32 b0 = (d & 2) ? a1 : a0;
-  u32 b1 = (d & 2) ? a3 : a2;
-  return (d & 4) ? b1 : b0;
-}
-
-// v >> (8 * sh) as a 16-byte little-endian value (sh in 0..15).
-__device__ __forceinline__ u32x4 shr_bytes3(u32x4 v, u32 sh) {
-  u32 t[8] = {v[0], v[1], v[2], v[3], 0u, 0u, 0u, 0u};
-  const u32 d = sh >> 2, b = sh & 3;
-  u32x4 r;
-  r[0] = alignbyte3(mux8v3(t, d + 1), mux8v3(t, d), b);
-  r[1] = alignbyte3(mux8v3(t, d + 2), mux8v3(t, d + 1), b);
-  r[2] = alignbyte3(d + 3 < 8 ? mux8v3(t, d + 3) : 0u, mux8v3(t, d + 2), b);
-  r[3] = alignbyte3(d + 4 < 8 ? mux8v3(t, d + 4) : 0u, mux8v3(t, d + 3), b);
-  return r;
-}
-
-// Store the first n (1..16) bytes of v at p exactly.
-__device__ __forceinline__ void store_exact3(u8* p, u32x4 v, u32 n) {
-  if (n == 16) { __builtin_memcpy(p, &v, 16); return; }
-  u64 lo = (u64)v[0] | ((u64)v[1] << 32);
-  u64 hi = (u64)v[2] | ((u64)v[3] << 32);
-  if (n & 8) { stu64(p, lo); p += 8; lo = hi; }
-  if (n & 4) { stu32(p, (u32)lo); p += 4; lo >>= 32; }
-  if (n & 2) { u16 s = (u16)lo; __builtin_memcpy(p, &s, 2); p += 2; lo >>= 16; }
-  if (n & 1) { *p = (u8)lo; }
-}
-
-__device__ __forceinline__ int parse_header3(const u8* ip, u32 n, bool strict, u32* ulen) {
-  u32 r = 0;
-  for (int i = 0; i < 5; ++i) {
-    if ((u32)i >= n) return 0;
-    u32 c = ip[i];
-    r |= (c & 0x7fu) << (7 * i);
-    if (c < 128) {
-      if (strict && i == 4 && c >= 16) return 0;
-      *ulen = r;
-      return i + 1;
-    }
-  }
-  return 0;
-}
-
-// v_perm selector for output byte t of a pattern of period `off`, expanded to
-// 16 bytes (see expand_pattern).
-__device__ __forceinline__ u32 pat_sel_byte(u32 off, u32 t) {
-  if (off <= 8) return t % off;                  // (p1:p0)
-  if (t < 8) return t;                           // (p1:p0), t < off
-  if (t < 12) return t < off ? 4 + (t - 8) : t - off;        // (p2:p0)
-  if (t < off) return 4 + (t - 12);                           // (p3:p0)
-  return t - off;                                // (p1:p0) if off <= 12, else (p3:p0) low bytes
-}
-
-// X[t] = P[t mod off], t < 16, for a pattern P of period off (1..15) whose
-// first `off` bytes are valid.  Pieces of a pattern copy are a multiple of
-// `off` long, so every piece stores this same X.
-__device__ __forceinline__ u32x4 expand_pattern(u32x4 p, u32 off, const u32x4* sel_tab) {
-  const u32x4 s = sel_tab[off];
-  u32x4 x;
-  x[0] = __builtin_amdgcn_perm(p[1], p[0], s[0]);
-  x[1] = __builtin_amdgcn_perm(p[1], p[0], s[1]);
-  x[2] = __builtin_amdgcn_perm(off <= 8 ? p[1] : p[2], p[0], s[2]);
-  x[3] = __builtin_amdgcn_perm(off <= 12 ? p[1] : p[3], p[0], s[3]);
-  return x;
-}
-
-// (16 / off) * off - 1 for off = 1..15, as nibbles: the piece length of a
-// pattern copy.
-__host__ __device__ constexpr u64 pat_step_nibbles() {
-  u64 k = 0;
-  for (u32 off = 1; off < 16; ++off) k |= (u64)((16 / off) * off - 1) << (4 * off);
-  return k;
-}
-constexpr u64 kPatStep = pat_step_nibbles();
-
 }  // namespace
 
 __global__ __launch_bounds__(64) void decode_pipe_kernel(
@@ -155,18 +71,15 @@ __global__ __launch_bounds__(64) void decode_pipe_kernel(
   __shared__ u32x4 sel_tab[16];
 
   const u32 lane = threadIdx.x;
-  {
-    const u32 off = lane >> 2, q = lane & 3;
-    u32 s = 0;
-    if (off > 0)
-      for (u32 r = 0; r < 4; ++r) s |= pat_sel_byte(off, 4 * q + r) << (8 * r);
-    reinterpret_cast<u32*>(sel_tab)[lane] = s;
-  }
+  init_pattern_table(sel_tab, lane);
   __syncthreads();
 
   const bool strict = flags & 2u;
   const u32 m = blockIdx.x * blockDim.x + lane;
-  const bool valid_msg = m < n_msgs;
+  // FSG_INTERNAL_FALLBACK_ONLY: decode only the messages the two-pass decoder
+  // (v4) left to this kernel (status kNeedFallback), leave the rest alone.
+  const bool fallback_only = flags & kFlagFallbackOnly;
+  const bool valid_msg = m < n_msgs && (!fallback_only || status_out[m] == kNeedFallback);
 
   // ---- message setup (header, slot check)
   i32 status = kOk;  // < 0: parsing
@@ -177,7 +90,7 @@ __global__ __launch_bounds__(64) void decode_pipe_kernel(
     ib = in + in_off[m];
     n_in = in_len[m];
     u32 ulen = 0;
-    const int h = parse_header3(ib, n_in, strict, &ulen);
+    const int h = parse_varint_header(ib, n_in, strict, &ulen);
     if (h == 0) { status = kBadHeader; out_len[m] = 0; }
     else {
       out_len[m] = ulen;
@@ -262,7 +175,7 @@ __global__ __launch_bounds__(64) void decode_pipe_kernel(
       const bool inwin = (P + 5 <= 16 * wend) || wend > last_chunk;
       const u32 dw = (P >> 2) & (kRingDwords - 1), bsh = P & 3;
       const u32 lo = ring[dw * kWave + lane], hi = ring[(dw + 1) * kWave + lane];
-      const u32 t0 = alignbyte3(hi, lo, bsh);       // bytes ip..ip+3
+      const u32 t0 = alignbyte(hi, lo, bsh);       // bytes ip..ip+3
       const u32 b4 = (hi >> (8 * bsh)) & 0xffu;      // byte ip+4
       const u32 c = t0 & 0xffu;
       const u32 type = c & 3;
@@ -294,7 +207,7 @@ __global__ __launch_bounds__(64) void decode_pipe_kernel(
       const u32 tkind = is_lit ? kKindLit : (small ? kKindPat : kKindCopy);
       kind = take ? tkind : kind;
       poff = take ? (small ? coff : 0u) : poff;
-      pstep = take ? (small ? (u32)((kPatStep >> (4 * coff)) & 15u) + 1u : 16u) : pstep;
+      pstep = take ? (small ? pat_step(coff) : 16u) : pstep;
       src = take ? (is_lit ? ip + 1 + nb : op - coff) : src;
       rem = take ? len : rem;
       ip = take ? ip + 1 + nb + (is_lit ? len : 0u) : ip;
@@ -353,7 +266,7 @@ __global__ __launch_bounds__(64) void decode_pipe_kernel(
     if (__any(any_shift)) {
 #pragma unroll
       for (int j = 0; j < kP3; ++j)
-        if (m_shf(rm_prev[j])) data[j] = shr_bytes3(data[j], m_shf(rm_prev[j]));
+        if (m_shf(rm_prev[j])) data[j] = shr_bytes(data[j], m_shf(rm_prev[j]));
     }
     if (__any(any_pat)) {
 #pragma unroll
@@ -373,7 +286,7 @@ __global__ __launch_bounds__(64) void decode_pipe_kernel(
 #pragma unroll
       for (int j = 0; j < kP3; ++j) {
         const u32 mm = rm_prev[j];
-        if (m_cnt(mm) && m_exact(mm)) store_exact3(ob + dsts[j], data[j], m_cnt(mm));
+        if (m_cnt(mm) && m_exact(mm)) store_exact(ob + dsts[j], data[j], m_cnt(mm));
       }
     }
 

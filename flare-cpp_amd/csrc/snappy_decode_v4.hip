@@ -1,0 +1,462 @@
+// snappy_decode_v4.hip -- two-pass Snappy decode for gfx950: a lane-per-message
+// index pass, then a wave-per-message execution pass.
+//
+// Why two passes.  The lane-per-message decoders (v1-v3) give a 65,536 x
+// 64 KiB batch exactly one wave per SIMD, and every piece load/store of a wave
+// instruction touches 64 unrelated cache lines.  The only serial part of Snappy
+// decode is finding the tag boundaries (each tag's length is in its first
+// bytes); everything else -- output offsets (a prefix sum), literal bytes and
+// most copy sources -- is data-parallel.  So:
+//
+//   pass 1, index_kernel (one LANE per message): the reference's tag walk
+//     (SnappyDecompressor::DecompressAllTags, /root/reference/flare/io/snappy/
+//     snappy.cc:716-787, with the writer checks of :1141-1227 / :1331-1481)
+//     without touching output.  It produces the final per-message status and
+//     a tag-start bitmap over the compressed bytes (bit p = a tag starts at
+//     compressed offset p), 1/8 of the input size.  Pure VALU + LDS ring
+//     reads; each lane reads its own input once.
+//
+//   pass 2, exec_kernel (one WAVE per message, only status-OK messages):
+//     walks the bitmap, takes up to 64 tags per group (one per lane), decodes
+//     them, prefix-sums their output lengths, cuts them into <= 16-byte pieces
+//     (one piece per lane) and executes the pieces in dependency rounds: a
+//     piece runs once every byte it reads precedes the first unfinished piece
+//     of the group.  Literal pieces and copies from before the group run in
+//     round 1; text needs ~5 rounds per 64-tag group.  The 64 lanes of a
+//     piece instruction touch a few neighbouring lines of one message, so the
+//     loads/stores coalesce, and 4 waves per workgroup / up to 8 per SIMD hide
+//     the latency.  Literals longer than 64 bytes are copied by the whole wave,
+//     1 KiB per instruction.
+//
+// Rounds rely on the in-order processing of one wave's vector memory
+// instructions: a round's loads are issued after the previous round's stores
+// (same wave), so they observe them, exactly as v3's batches do.
+//
+// A message whose bitmap does not fit the workspace gets status kNeedFallback
+// in pass 1 and is decoded by the v3 kernel (kFlagFallbackOnly).
+#include "snappy_pieces.h"
+
+namespace fsg {
+
+namespace {
+
+// ---- pass 1 geometry (per-lane LDS ring of input chunks, as v3)
+constexpr int kIdxTags = 16;                 // tags per iteration
+constexpr u32 kRingChunks = 16;              // 16-byte chunks per lane (256 B)
+constexpr u32 kRingDwords = kRingChunks * 4;
+constexpr u32 kAhead = 5;                    // chunks prefetched per iteration
+
+// ---- pass 2 geometry
+constexpr u32 kWavesPerBlock = 4;
+constexpr u32 kTagRing = 512;                // tag positions per wave (LDS)
+constexpr u32 kFillWords = 16;               // bitmap words per fill (512 input bytes)
+constexpr u32 kMaxPieces = 64;
+
+__device__ u32x4 g_dummy_chunk[1];
+
+__device__ __forceinline__ u32 wave_incl_scan(u32 v) {
+  const u32 lane = __lane_id();
+#pragma unroll
+  for (u32 d = 1; d < 64; d <<= 1) {
+    const u32 t = __shfl_up(v, d, 64);
+    v += lane >= d ? t : 0u;
+  }
+  return v;
+}
+
+__device__ __forceinline__ u32 readlane(u32 v, u32 l) {
+  return (u32)__builtin_amdgcn_readlane((int)v, (int)l);
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 16 bytes of a message buffer at `off`, never touching bytes outside
+// [-(bal), limit) (see clamped_origin).
+__device__ __forceinline__ u32x4 load16_clamped(const u8* base, u32 off, u32 limit, u32 bal) {
+  const int a = clamped_origin(off, limit, bal);
+  u32x4 v;
+  __builtin_memcpy(&v, base + a, 16);
+  const u32 sh = (u32)((int)off - a);
+  return sh ? shr_bytes(v, sh) : v;
+}
+
+// ceil(len / step) for a pattern copy: len <= 64 and step >= 9 (pat_step of
+// offsets 1..15), so the answer is 1..8 -- counted instead of divided.
+__device__ __forceinline__ u32 pattern_pieces(u32 len, u32 step) {
+  u32 pc = 1;
+#pragma unroll
+  for (u32 k = 1; k < 8; ++k) pc += len > k * step ? 1u : 0u;
+  return pc;
+}
+
+}  // namespace
+
+// ===========================================================================
+// Pass 1: index + validate.  One lane per message.
+// ===========================================================================
+__global__ __launch_bounds__(64) void index_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off,
+    const u32* __restrict__ in_len, u32 n_msgs, const u32* __restrict__ out_cap,
+    u32* __restrict__ out_len, i32* __restrict__ status_out, u32 flags,
+    u32* __restrict__ bm_counter, u32* __restrict__ bm_base_out,
+    u32* __restrict__ bitmap, u64 bm_capacity_words) {
+  // [dword][lane]; dword 64 = copy of dword 0; 65..68 absorb unused prefetches
+  __shared__ u32 ring[(kRingDwords + 5) * kWave];
+
+  const u32 lane = threadIdx.x;
+  const bool strict = flags & 2u;
+  const bool validate = flags & 1u;
+  const u32 m = blockIdx.x * blockDim.x + lane;
+  const bool valid_msg = m < n_msgs;
+
+  i32 status = kOk;  // < 0: parsing
+  const u8* ib = in;
+  u32 n_in = 0, expected = 0, ip = 0;
+  if (valid_msg) {
+    ib = in + in_off[m];
+    n_in = in_len[m];
+    u32 ulen = 0;
+    const int h = parse_varint_header(ib, n_in, strict, &ulen);
+    if (h == 0) {
+      status = kBadHeader;
+      out_len[m] = 0;
+    } else {
+      out_len[m] = ulen;
+      expected = ulen;
+      ip = (u32)h;
+      status = (!validate && ulen > out_cap[m]) ? kSlotTooSmall : -1;
+    }
+  }
+
+  // ---- bitmap allocation: round_up(ceil(n_in / 32), 4) words, bump-allocated
+  // per wave (order is irrelevant; bases stay 16-byte aligned)
+  u32 bm_base = 0;
+  if (bitmap) {
+    const u32 words = status < 0 ? (((n_in + 31) >> 5) + 3) & ~3u : 0u;
+    const u32 incl = wave_incl_scan(words);
+    const u32 total = readlane(incl, 63);
+    u32 base0 = 0;
+    if (lane == 0 && total) base0 = atomicAdd(bm_counter, total);
+    base0 = readlane(base0, 0);
+    bm_base = base0 + incl - words;
+    if (status < 0 && (u64)bm_base + words > bm_capacity_words) status = kNeedFallback;
+    if (valid_msg) bm_base_out[m] = bm_base;
+  }
+  u32* bm = bitmap ? bitmap + bm_base : nullptr;
+
+  const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
+  const u8* abase = ib - ibal;
+  const u32 last_chunk = n_in ? (ibal + n_in - 1) >> 4 : 0u;
+
+  u32 wend = 0, iend = 0;
+  auto ring_write = [&](u32 k, u32x4 v, bool live) {
+    const u32 d = live ? (k & (kRingChunks - 1)) * 4 : kRingDwords + 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ring[(d + i) * kWave + lane] = v[i];
+    ring[(d == 0 ? kRingDwords : kRingDwords + 1) * kWave + lane] = v[0];
+  };
+  if (status < 0) {
+    u32x4 c0[4];
+#pragma unroll
+    for (u32 c = 0; c < 4; ++c) {
+      const u32 k = c <= last_chunk ? c : last_chunk;
+      c0[c] = *reinterpret_cast<const u32x4*>(abase + 16 * k);
+    }
+#pragma unroll
+    for (u32 c = 0; c < 4; ++c) ring_write(c, c0[c], c <= last_chunk);
+    wend = iend = (last_chunk + 1 < 4) ? last_chunk + 1 : 4;
+  }
+
+  u32 op = 0;
+  // bitmap accumulator: words of the current 128-byte group `cg`
+  u32 acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0, cg = 0;
+  auto flush = [&]() {
+    if (acc0 | acc1 | acc2 | acc3)
+      *reinterpret_cast<u32x4*>(bm + 4 * cg) = u32x4{acc0, acc1, acc2, acc3};
+    acc0 = acc1 = acc2 = acc3 = 0;
+  };
+
+  u32x4 g[kAhead];
+#pragma unroll
+  for (u32 c = 0; c < kAhead; ++c) g[c] = u32x4{0, 0, 0, 0};
+  u32 gk_w = 0, gn_w = 0;
+
+  __builtin_amdgcn_s_waitcnt(0);
+  bool more = __any(status < 0);
+  while (more) {
+    // ---------- parse up to kIdxTags tags from the ring
+#pragma unroll
+    for (int j = 0; j < kIdxTags; ++j) {
+      const bool need = status < 0;
+      const bool eof = need && ip == n_in;  // RefillTag eof
+      const u32 P = ip + ibal;
+      const bool inwin = (P + 5 <= 16 * wend) || wend > last_chunk;
+      const u32 dw = (P >> 2) & (kRingDwords - 1), bsh = P & 3;
+      const u32 lo = ring[dw * kWave + lane], hi = ring[(dw + 1) * kWave + lane];
+      const u32 t0 = alignbyte(hi, lo, bsh);     // bytes ip..ip+3
+      const u32 b4 = (hi >> (8 * bsh)) & 0xffu;  // byte ip+4
+      const u32 c = t0 & 0xffu;
+      const u32 type = c & 3;
+      const bool is_lit = type == 0;
+      const u32 l0 = (c >> 2) + 1;
+      const bool longlit = is_lit && l0 >= 61;   // 1..4 length bytes (:744-750)
+      const u32 nbl = longlit ? l0 - 60 : 0u;
+      const u32 ext = (b4 << 24) | (t0 >> 8);
+      const u32 msk = nbl >= 4 ? 0xffffffffu : ((1u << (8 * nbl)) - 1u);
+      const u32 litlen = longlit ? (ext & msk) + 1u : l0;  // uint32 wrap: 0xffffffff+1 == 0
+      const u32 nb = is_lit ? nbl : (type == 1 ? 1u : (type == 2 ? 2u : 4u));
+      const u32 clen = type == 1 ? 4 + ((c >> 2) & 7) : l0;
+      const u32 coff = type == 1 ? (((c >> 5) << 8) | ((t0 >> 8) & 0xffu))
+                                 : (type == 2 ? ((t0 >> 8) & 0xffffu) : ext);
+      const u32 len = is_lit ? litlen : clen;
+      const u32 avail = n_in - ip - 1;
+      const u32 space = expected - op;
+      const bool bad = avail < nb ||
+                       (is_lit ? (avail - nb < len || space < len)     // :761, writer overrun
+                               : (coff - 1u >= op || space < len));    // :1200 / :1410,1466
+      const bool hdr = need && !eof && inwin;
+      status = eof ? (op == expected ? kOk : kCorrupt) : ((hdr && bad) ? kCorrupt : status);
+      const bool take = hdr && !bad;
+      if (bm && take) {
+        const u32 gi = ip >> 7;
+        if (gi != cg) { flush(); cg = gi; }
+        const u32 bit = 1u << (ip & 31), wsel = (ip >> 5) & 3;
+        acc0 |= wsel == 0 ? bit : 0u;
+        acc1 |= wsel == 1 ? bit : 0u;
+        acc2 |= wsel == 2 ? bit : 0u;
+        acc3 |= wsel == 3 ? bit : 0u;
+      }
+      ip = take ? ip + 1 + nb + (is_lit ? len : 0u) : ip;
+      op = take ? op + len : op;
+    }
+
+    // ---------- land the chunks loaded last iteration
+#pragma unroll
+    for (u32 c = 0; c < kAhead; ++c) ring_write(gk_w + c, g[c], c < gn_w);
+    wend = gn_w ? gk_w + gn_w : wend;
+
+    // ---------- prefetch from the parse position
+    {
+      const u32 P = ip + ibal;
+      const u32 pc = P >> 4;
+      const u32 base = pc >= iend ? pc : iend;  // a long literal jumped past the ring: restart
+      u32 cnt = 0;
+#pragma unroll
+      for (u32 c = 0; c < kAhead; ++c) {
+        const u32 k = base + c;
+        const bool ok = status < 0 && k <= last_chunk && k <= pc + (kRingChunks - 1);
+        cnt += ok ? 1u : 0u;
+        const u32 kk = k <= last_chunk ? k : last_chunk;
+        g[c] = *reinterpret_cast<const u32x4*>(n_in ? abase + 16 * kk
+                                                    : reinterpret_cast<const u8*>(g_dummy_chunk));
+      }
+      iend = cnt ? base + cnt : iend;
+      gk_w = base;
+      gn_w = cnt;
+    }
+    more = __any(status < 0);
+  }
+  if (bm && status == kOk) flush();
+  if (valid_msg) status_out[m] = status;
+}
+
+// ===========================================================================
+// Pass 2: execute.  One wave per status-OK message.
+// ===========================================================================
+__global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off,
+    const u32* __restrict__ in_len, u32 n_msgs, u8* out,
+    const u64* __restrict__ out_off, const u32* __restrict__ out_len,
+    const i32* __restrict__ status, const u32* __restrict__ bm_base,
+    const u32* __restrict__ bitmap) {
+  __shared__ u32 ring_s[kWavesPerBlock][kTagRing];
+  __shared__ u8 pmap_s[kWavesPerBlock][kMaxPieces];
+  __shared__ u32x4 sel_tab[16];
+
+  if (threadIdx.x < 64) init_pattern_table(sel_tab, threadIdx.x);
+  __syncthreads();
+
+  const u32 wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const u32 m = blockIdx.x * kWavesPerBlock + wv;
+  if (m >= n_msgs) return;
+  if (status[m] != kOk) return;
+
+  const u32 n_in = in_len[m];
+  const u32 expected = out_len[m];
+  const u8* ib = in + in_off[m];
+  u8* ob = out + out_off[m];
+  const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
+  const u32 obal = (u32)(reinterpret_cast<uintptr_t>(ob) & 15);
+  const u32* bm = bitmap + bm_base[m];
+  const u32 nwords = (n_in + 31) >> 5;
+  u32* ring = ring_s[wv];
+  u8* pmap = pmap_s[wv];
+
+  u32 head = 0, tail = 0, scan = 0, op = 0;
+  u32 bmw = (lane < kFillWords && lane < nwords) ? bm[lane] : 0u;  // next fill, prefetched
+  // tag bytes prefetched for ring entries [pf_head, pf_head + pf_cnt)
+  u32 pf_head = 0xffffffffu, pf_cnt = 0;
+  u32x4 tv = u32x4{0, 0, 0, 0};
+
+  for (;;) {
+    // ---------- refill the tag ring from the bitmap (keeps >= 64 tags ahead)
+    if (tail - head < 2 * kMaxPieces && scan < nwords) {
+      const u32 cnt = __builtin_popcount(bmw);
+      const u32 incl = wave_incl_scan(cnt);
+      u32 slot = tail + incl - cnt;
+      u32 word = bmw;
+      const u32 bitbase = (scan + lane) * 32;
+      while (word) {
+        const u32 b = __builtin_ctz(word);
+        ring[slot & (kTagRing - 1)] = bitbase + b;
+        ++slot;
+        word &= word - 1;
+      }
+      tail += readlane(incl, 63);
+      scan += kFillWords;
+      bmw = (lane < kFillWords && scan + lane < nwords) ? bm[scan + lane] : 0u;
+      wave_lds_fence();
+      continue;
+    }
+    const u32 avail = tail - head;
+    if (avail == 0) break;
+    const u32 take0 = avail < 64 ? avail : 64u;
+    const bool valid = lane < take0;
+    const u32 pos = valid ? ring[(head + lane) & (kTagRing - 1)] : 0u;
+    if (pf_head != head || pf_cnt < take0)
+      tv = valid ? load16_clamped(ib, pos, n_in, ibal) : u32x4{0, 0, 0, 0};
+
+    // ---------- decode one tag per lane (checked by pass 1)
+    const u32 t0 = tv[0], t1 = tv[1];
+    const u32 c = t0 & 0xffu;
+    const u32 type = c & 3;
+    const bool is_lit = type == 0;
+    const u32 l0 = (c >> 2) + 1;
+    const bool longlit = is_lit && l0 >= 61;
+    const u32 nbl = longlit ? l0 - 60 : 0u;
+    const u32 ext = (t0 >> 8) | (t1 << 24);
+    const u32 msk = nbl >= 4 ? 0xffffffffu : ((1u << (8 * nbl)) - 1u);
+    const u32 litlen = longlit ? (ext & msk) + 1u : l0;
+    const u32 nb = is_lit ? nbl : (type == 1 ? 1u : (type == 2 ? 2u : 4u));
+    const u32 clen = type == 1 ? 4 + ((c >> 2) & 7) : l0;
+    const u32 coff = type == 1 ? (((c >> 5) << 8) | ((t0 >> 8) & 0xffu))
+                               : (type == 2 ? ((t0 >> 8) & 0xffffu) : ext);
+    const u32 len = is_lit ? litlen : clen;
+    const u32 lsrc = pos + 1 + nb;
+
+    const u64 bigm = __ballot(valid && is_lit && len > 64);
+    if (bigm & 1ull) {
+      // ---------- long literal: the whole wave copies it, 1 KiB per step
+      const u32 L = readlane(len, 0), S = readlane(lsrc, 0);
+      for (u32 k = lane * 16; k < L; k += 1024) {
+        const u32 n = L - k < 16 ? L - k : 16u;
+        store_exact(ob + op + k, load16_clamped(ib, S + k, n_in, ibal), n);
+      }
+      op += L;
+      head += 1;
+      pf_head = 0xffffffffu;
+      continue;
+    }
+    const u32 take = bigm ? (u32)__builtin_ctzll(bigm) : take0;
+    const bool v = lane < take;
+
+    // ---------- pieces: <= 16 bytes each, one per lane
+    const bool pat = !is_lit && coff < 16;
+    const u32 step = pat ? pat_step(coff) : 16u;
+    const u32 pc = v ? (pat ? pattern_pieces(len, step) : (len + 15) >> 4) : 0u;
+    const u32 lv = v ? len : 0u;
+    const u32 incl = wave_incl_scan(pc | (lv << 16));
+    const u32 incl_pc = incl & 0xffffu, excl_pc = incl_pc - pc;
+    const bool fits = v && incl_pc <= kMaxPieces;
+    const u32 k_tags = (u32)__builtin_popcountll(__ballot(fits));
+    const u32 t_op = op + (incl >> 16) - lv;
+    const u32 tot_pc = readlane(incl_pc, k_tags - 1);
+    const u32 tot_len = readlane(incl >> 16, k_tags - 1);
+
+    // ---------- prefetch the next group's tag bytes (lands during the rounds)
+    {
+      const u32 nh = head + k_tags;
+      const u32 na = tail - nh;
+      const u32 ncnt = na < 64 ? na : 64u;
+      if (lane < ncnt) {
+        const u32 npos = ring[(nh + lane) & (kTagRing - 1)];
+        tv = load16_clamped(ib, npos, n_in, ibal);
+      }
+      pf_head = nh;
+      pf_cnt = ncnt;
+    }
+
+    if (fits)
+      for (u32 p = 0; p < pc; ++p) pmap[excl_pc + p] = (u8)lane;
+    wave_lds_fence();
+    const bool has = lane < tot_pc;
+    const u32 t = has ? pmap[lane] : 0u;
+    const u32 kind = is_lit ? 0u : (pat ? 2u : 1u);
+    const u32 A = t_op;
+    const u32 B = len | (excl_pc << 8) | (kind << 16) | ((pat ? coff : 0u) << 20);
+    const u32 C = is_lit ? lsrc : t_op - coff;
+    const u32 At = __shfl(A, t, 64), Bt = __shfl(B, t, 64), Ct = __shfl(C, t, 64);
+    const u32 lenT = Bt & 0xffu, exT = (Bt >> 8) & 0xffu, kT = (Bt >> 16) & 3u, offT = Bt >> 20;
+    const u32 stepT = kT == 2 ? pat_step(offT) : 16u;
+    const u32 qs = (lane - exT) * stepT;
+    const u32 dst = At + qs;
+    const u32 n = lenT - qs < stepT ? lenT - qs : stepT;
+    const u32 src = kT == 2 ? Ct : Ct + qs;
+    const u32 need_end = kT == 0 ? 0u : (kT == 2 ? At : src + n);
+
+    // ---------- dependency rounds
+    bool done = !has;
+    for (;;) {
+      const u64 nd = __ballot(!done);
+      if (!nd) break;
+      const u32 wm = readlane(dst, (u32)__builtin_ctzll(nd));
+      const bool ready = !done && need_end <= wm;
+      if (ready) {
+        u32x4 x = kT == 0 ? load16_clamped(ib, src, n_in, ibal)
+                          : load16_clamped(ob, src, expected, obal);
+        if (kT == 2) x = expand_pattern(x, offT, sel_tab);
+        store_exact(ob + dst, x, n);
+      }
+      done = done || ready;
+    }
+    op += tot_len;
+    head += k_tags;
+  }
+}
+
+size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
+  const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
+  const u64 words = total_in_bytes / 32 + 4ull * n_msgs + 64;
+  return (size_t)(256 + base_bytes + 4 * words);
+}
+
+hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
+                            u32 n_msgs, u8* out, const u64* out_off,
+                            const u32* out_cap, u32* out_len, i32* status,
+                            u32 flags, void* ws, size_t ws_bytes, hipStream_t stream) {
+  if (n_msgs == 0) return hipSuccess;
+  u8* w = static_cast<u8*>(ws);
+  const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
+  u32* counter = reinterpret_cast<u32*>(w);
+  u32* bm_base = reinterpret_cast<u32*>(w + 256);
+  u32* bitmap = reinterpret_cast<u32*>(w + 256 + base_bytes);
+  const u64 cap_words = (ws_bytes - 256 - base_bytes) / 4;
+  // zero the counter and the bitmap (pass 1 writes only groups holding tags)
+  hipError_t e = hipMemsetAsync(counter, 0, 4, stream);
+  if (e == hipSuccess) e = hipMemsetAsync(bitmap, 0, cap_words * 4, stream);
+  if (e != hipSuccess) return e;
+  index_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out_cap, out_len,
+                                                      status, flags, counter, bm_base, bitmap,
+                                                      cap_words);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  exec_kernel<<<(n_msgs + kWavesPerBlock - 1) / kWavesPerBlock, kWavesPerBlock * 64, 0, stream>>>(
+      in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return hipSuccess;
+}
+
+}  // namespace fsg

@@ -27,6 +27,10 @@ constexpr i32 kOk = 0;
 constexpr i32 kCorrupt = 1;
 constexpr i32 kBadHeader = 2;
 constexpr i32 kSlotTooSmall = 3;
+// Internal: message not indexed by the two-pass decoder (its bitmap did not
+// fit the workspace); finished by the v3 kernel under kFlagFallbackOnly.
+constexpr i32 kNeedFallback = 0x40000000;
+constexpr u32 kFlagFallbackOnly = 0x80000000u;
 
 __host__ __device__ inline u64 max_compressed_length(u64 n) {
   return 32 + n + n / 6;  // snappy.cc:55-77

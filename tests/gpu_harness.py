@@ -44,7 +44,10 @@ class GpuCodec:
         st = d_st.cpu().numpy()[:n]
         return [out[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() for i in range(n)], st
 
-    def decompress(self, comps: list[bytes], caps: list[int], flags: int = 0):
+    def decompress(self, comps: list[bytes], caps: list[int], flags: int = 0,
+                   ws_total_in: int | None = None):
+        """ws_total_in: input size the workspace is sized for (default: the
+        real packed size; smaller values force the v4 fallback path)."""
         torch = self.torch
         b = fsg.Batch.from_list(comps)
         n = len(b)
@@ -53,7 +56,8 @@ class GpuCodec:
         d_out = torch.zeros(tot, dtype=torch.uint8, device="cuda")
         d_ol = empty(n, torch.int32)
         d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
-        ws = self.codec.decompress_workspace(n) if self.use_workspace else None
+        total_in = int(b.data.size) if ws_total_in is None else ws_total_in
+        ws = self.codec.decompress_workspace(n, total_in) if self.use_workspace else None
         self.codec.decompress(dev(b.data), dev(b.offsets), dev(b.lens), n, d_out, dev(oo), dev(caps),
                               d_ol, d_st, flags=flags, workspace=ws)
         torch.cuda.synchronize()

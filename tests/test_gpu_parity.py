@@ -116,7 +116,9 @@ def test_randomized_against_oracle(gpu, oracle):
     assert (st == 0).all() and all(o == x for o, x in zip(outs, items))
 
 
-def test_decode_fuzz_against_oracle(gpu, oracle):
+@pytest.mark.parametrize("variant", [0, 3, 4])
+def test_decode_fuzz_against_oracle(gpu, oracle, variant):
+    gpu.codec.select_kernels(variant, 0)
     rng = np.random.default_rng(9)
     srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (64, 700, 9000, 70000)]
     comps, caps = [], []
@@ -138,12 +140,13 @@ def test_decode_fuzz_against_oracle(gpu, oracle):
             assert s in (fsg.FSG_CORRUPT, fsg.FSG_BAD_HEADER)
         else:
             assert s == fsg.FSG_OK and o[:ulen] == ref
+    gpu.codec.select_kernels(0, 0)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
 def test_kernel_variants_agree(gpu, oracle, variant):
     """Every generation of kernels gives the oracle's bytes and statuses."""
-    gpu.codec.select_kernels(variant, variant)
+    gpu.codec.select_kernels(variant, min(variant, 3))
     try:
         vecs = json.loads((GOLDEN / "vectors.json").read_text())
         datas = [build_input(v) for v in vecs if v["input_len"] <= 200000]
@@ -242,7 +245,7 @@ def _synthetic_stream(rng, target):
     return bytes(hdr) + b"".join(body), bytes(out)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_pattern_copies_and_ring_jumps(gpu, oracle, variant):
     """Hand-built streams: every small offset/length combination, COPY_4 and
     long literals, at output ends of every alignment; decoded bytes equal the
@@ -260,5 +263,27 @@ def test_pattern_copies_and_ring_jumps(gpu, oracle, variant):
             ok, ulen, ref = oracle.uncompress(c, cap=len(raw))
             assert ok and ref == raw, i
             assert s == fsg.FSG_OK and o == raw, i
+    finally:
+        gpu.codec.select_kernels(0, 0)
+
+
+@pytest.mark.parametrize("total_in", [0, 1, 4096, 60000])
+def test_two_pass_workspace_fallback(gpu, oracle, total_in):
+    """v4 with a workspace sized for less input than the batch holds: the
+    messages whose tag bitmap does not fit are finished by the v3 kernel
+    (internal status kNeedFallback); every byte and status still matches."""
+    gpu.codec.select_kernels(4, 0)
+    try:
+        rng = np.random.default_rng(77)
+        items = [fsg.make_batch(fsg.KIND_TEXT if i % 3 else fsg.KIND_RANDOM,
+                                [int(rng.integers(0, 70000))], first_index=i).item(0) for i in range(200)]
+        comps = [oracle.compress(x) for x in items]
+        comps[5] = comps[5][:-2]
+        outs, ol, st = gpu.decompress(comps, [len(x) for x in items], ws_total_in=total_in)
+        for i, (x, c, o, s) in enumerate(zip(items, comps, outs, st)):
+            ok, ulen, ref = oracle.uncompress(c, cap=len(x))
+            assert (s == fsg.FSG_OK) == bool(ok), (i, s)
+            if ok:
+                assert o == x, i
     finally:
         gpu.codec.select_kernels(0, 0)
