@@ -266,7 +266,33 @@ __global__ __launch_bounds__(64) void index_kernel(
 
 // ===========================================================================
 // Pass 2: execute.  One wave per status-OK message.
+//
+// Output is assembled in a per-wave LDS window `sb` (kWindow bytes) holding
+// output positions [sbase, sbase + kWindow); sbase is kept congruent to the
+// slot's address modulo 16 so window offsets and global addresses share
+// 16-byte alignment.  Per group of <= 64 pieces:
+//   round A   literal pieces (input bytes) and far copies (source before the
+//             window, already stored) load from global memory -- one round
+//             trip, all independent -- and land in the window;
+//   rounds B  near copies (source inside the window) resolve in LDS in
+//             dependency rounds;
+//   flush     completed 16-byte blocks go to global memory, 1 KiB per wave
+//             instruction.
+// The window slides (keeping >= 2 KiB of history) when a group would overrun
+// it.  Literals longer than 64 bytes bypass it: the wave copies them
+// global-to-global, 1 KiB per instruction.
 // ===========================================================================
+namespace {
+constexpr u32 kWindow = 4096;  // LDS output window per wave
+constexpr u32 kKeep = 2048;    // history kept when the window slides
+
+__device__ __forceinline__ u32x4 lds_read16(const u8* p) {
+  u32x4 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+}  // namespace
+
 __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, u8* out,
@@ -275,6 +301,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     const u32* __restrict__ bitmap) {
   __shared__ u32 ring_s[kWavesPerBlock][kTagRing];
   __shared__ u8 pmap_s[kWavesPerBlock][kMaxPieces];
+  __shared__ __attribute__((aligned(16))) u8 sb_s[kWavesPerBlock][kWindow + 32];
   __shared__ u32x4 sel_tab[16];
 
   if (threadIdx.x < 64) init_pattern_table(sel_tab, threadIdx.x);
@@ -295,12 +322,32 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
   const u32 nwords = (n_in + 31) >> 5;
   u32* ring = ring_s[wv];
   u8* pmap = pmap_s[wv];
+  u8* sb = sb_s[wv];
 
   u32 head = 0, tail = 0, scan = 0, op = 0;
+  int sbase = -(int)obal;  // output position of sb[0]
+  u32 flushed = 0;         // output [0, flushed) is in global memory
   u32 bmw = (lane < kFillWords && lane < nwords) ? bm[lane] : 0u;  // next fill, prefetched
-  // tag bytes prefetched for ring entries [pf_head, pf_head + pf_cnt)
-  u32 pf_head = 0xffffffffu, pf_cnt = 0;
+  u32 pf_head = 0xffffffffu, pf_cnt = 0;  // tag bytes prefetched for ring [pf_head, +pf_cnt)
   u32x4 tv = u32x4{0, 0, 0, 0};
+
+  // Store window bytes [flushed, fe) to the slot: one 16-byte block per lane,
+  // whole aligned blocks with one store, partial edge blocks exactly.
+  auto flush_to = [&](u32 fe) {
+    if (fe <= flushed) return;
+    const int b0 = (int)(((flushed + obal) & ~15u)) - (int)obal;  // block start <= flushed
+    for (int blk = b0 + 16 * (int)lane; blk < (int)fe; blk += 1024) {
+      const u32 lo = blk < (int)flushed ? flushed : (u32)blk;
+      const u32 hi = blk + 16 < (int)fe ? (u32)(blk + 16) : fe;
+      if (hi - lo == 16) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(sb + (blk - sbase));
+        __builtin_memcpy(ob + blk, &v, 16);
+      } else {
+        store_exact(ob + lo, lds_read16(sb + ((int)lo - sbase)), hi - lo);
+      }
+    }
+    flushed = fe;
+  };
 
   for (;;) {
     // ---------- refill the tag ring from the bitmap (keeps >= 64 tags ahead)
@@ -350,13 +397,28 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
 
     const u64 bigm = __ballot(valid && is_lit && len > 64);
     if (bigm & 1ull) {
-      // ---------- long literal: the whole wave copies it, 1 KiB per step
+      // ---------- long literal: written straight to the slot by the whole
+      // wave; the window restarts behind it
       const u32 L = readlane(len, 0), S = readlane(lsrc, 0);
+      flush_to(op);
       for (u32 k = lane * 16; k < L; k += 1024) {
         const u32 n = L - k < 16 ? L - k : 16u;
         store_exact(ob + op + k, load16_clamped(ib, S + k, n_in, ibal), n);
       }
       op += L;
+      flushed = op;
+      // The window restarts one block before the block holding op, so that
+      // >= 16 flushed bytes precede it (a copy reading before the window
+      // then reads only stored bytes); its head comes from the literal's tail.
+      sbase = (int)((op + obal) & ~15u) - (int)obal - 16;
+      if (lane < 2) {
+        const u32 lo = (u32)sbase + 16 * lane;
+        if (lo < op) {
+          const u32 cnt = op - lo < 16 ? op - lo : 16u;
+          store_exact(sb + 16 * lane, load16_clamped(ib, S + L - (op - lo), n_in, ibal), cnt);
+        }
+      }
+      wave_lds_fence();
       head += 1;
       pf_head = 0xffffffffu;
       continue;
@@ -377,7 +439,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     const u32 tot_pc = readlane(incl_pc, k_tags - 1);
     const u32 tot_len = readlane(incl >> 16, k_tags - 1);
 
-    // ---------- prefetch the next group's tag bytes (lands during the rounds)
+    // ---------- prefetch the next group's tag bytes (lands during this group)
     {
       const u32 nh = head + k_tags;
       const u32 na = tail - nh;
@@ -388,6 +450,21 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
       }
       pf_head = nh;
       pf_cnt = ncnt;
+    }
+
+    // ---------- slide the window if this group would overrun it
+    if (op + tot_len - sbase > kWindow) {
+      const int nsb = (int)(((op - kKeep + obal) & ~15u)) - (int)obal;
+      const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
+      for (u32 k = 0; k < keep; k += 1024) {
+        const u32 i = k + 16 * lane;
+        u32x4 x = u32x4{0, 0, 0, 0};
+        if (i < keep) x = *reinterpret_cast<const u32x4*>(sb + shift + i);
+        wave_lds_fence();
+        if (i < keep) *reinterpret_cast<u32x4*>(sb + i) = x;
+        wave_lds_fence();
+      }
+      sbase = nsb;
     }
 
     if (fits)
@@ -407,25 +484,41 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     const u32 n = lenT - qs < stepT ? lenT - qs : stepT;
     const u32 src = kT == 2 ? Ct : Ct + qs;
     const u32 need_end = kT == 0 ? 0u : (kT == 2 ? At : src + n);
+    u8* const wdst = sb + ((int)dst - sbase);
 
-    // ---------- dependency rounds
-    bool done = !has;
+    // ---------- round A: literal pieces and far copies, from global memory
+    const bool global_src = has && (kT == 0 || (int)src < sbase);
+    if (global_src) {
+      u32x4 x = kT == 0 ? load16_clamped(ib, src, n_in, ibal)
+                        : load16_clamped(ob, src, expected, obal);
+      if (kT == 2) x = expand_pattern(x, offT, sel_tab);
+      store_exact(wdst, x, n);
+    }
+    wave_lds_fence();
+
+    // ---------- rounds B: near copies, in LDS, in dependency order
+    bool done = !has || global_src;
     for (;;) {
       const u64 nd = __ballot(!done);
       if (!nd) break;
       const u32 wm = readlane(dst, (u32)__builtin_ctzll(nd));
       const bool ready = !done && need_end <= wm;
       if (ready) {
-        u32x4 x = kT == 0 ? load16_clamped(ib, src, n_in, ibal)
-                          : load16_clamped(ob, src, expected, obal);
+        u32x4 x = lds_read16(sb + ((int)src - sbase));
         if (kT == 2) x = expand_pattern(x, offT, sel_tab);
-        store_exact(ob + dst, x, n);
+        store_exact(wdst, x, n);
       }
+      wave_lds_fence();
       done = done || ready;
     }
     op += tot_len;
     head += k_tags;
+
+    // ---------- flush completed 16-byte blocks
+    const int fe = (int)((op + obal) & ~15u) - (int)obal;
+    if (fe > (int)flushed) flush_to((u32)fe);
   }
+  flush_to(expected);
 }
 
 size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
