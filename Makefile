@@ -57,3 +57,12 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all gpu host cpptests datagen oracle clean
+
+# Diagnostic build: exec_kernel phase stamps (s_memtime), never loaded by the
+# product path.  python tools/stamps.py runs it.
+stamps: $(LIB)/libflare_snappy_gpu_stamps.so
+$(LIB)/libflare_snappy_gpu_stamps.so: $(CSRC) $(CHDRS)
+	@mkdir -p $(LIB) build/stamps
+	for f in $(CSRC); do $(HIPCC) $(HIPFLAGS) -DFSG_STAMPS -c $$f -o build/stamps/$$(basename $$f .hip).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ build/stamps/*.o
+.PHONY: stamps

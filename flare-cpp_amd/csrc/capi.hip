@@ -194,7 +194,7 @@ int fsg_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
                                      (hipStream_t)stream),
                   "fsg_decompress_batch");
   const bool v4_fits = d_workspace && workspace_bytes >= fsg::decode_v4_workspace_bytes(n_msgs, 0);
-  if (forced == 4 && v4_fits) {
+  if ((forced == 0 || forced == 4) && v4_fits) {
     hipError_t e = fsg::launch_decode_v4(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
                                          d_out_cap, d_out_len, d_status, flags, d_workspace,
                                          workspace_bytes, (hipStream_t)stream);

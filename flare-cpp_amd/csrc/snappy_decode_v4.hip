@@ -54,6 +54,15 @@ constexpr u32 kMaxPieces = 64;
 
 __device__ u32x4 g_dummy_chunk[1];
 
+// Diagnostic build only (-DFSG_STAMPS): per-phase cycle totals of exec_kernel,
+// summed over waves, read back with fsg_debug_stamps.
+#ifdef FSG_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define STAMP(k) do { const u64 t_ = __builtin_amdgcn_s_memtime(); st_[k] += t_ - t_last_; t_last_ = t_; } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
 __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
   const u32 lane = __lane_id();
 #pragma unroll
@@ -324,6 +333,10 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
   u8* pmap = pmap_s[wv];
   u8* sb = sb_s[wv];
 
+#ifdef FSG_STAMPS
+  u64 st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 t_last_ = __builtin_amdgcn_s_memtime();
+#endif
   u32 head = 0, tail = 0, scan = 0, op = 0;
   int sbase = -(int)obal;  // output position of sb[0]
   u32 flushed = 0;         // output [0, flushed) is in global memory
@@ -367,6 +380,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
       scan += kFillWords;
       bmw = (lane < kFillWords && scan + lane < nwords) ? bm[scan + lane] : 0u;
       wave_lds_fence();
+      STAMP(0);
       continue;
     }
     const u32 avail = tail - head;
@@ -396,14 +410,25 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     const u32 lsrc = pos + 1 + nb;
 
     const u64 bigm = __ballot(valid && is_lit && len > 64);
+    STAMP(1);
     if (bigm & 1ull) {
       // ---------- long literal: written straight to the slot by the whole
       // wave; the window restarts behind it
       const u32 L = readlane(len, 0), S = readlane(lsrc, 0);
       flush_to(op);
-      for (u32 k = lane * 16; k < L; k += 1024) {
-        const u32 n = L - k < 16 ? L - k : 16u;
-        store_exact(ob + op + k, load16_clamped(ib, S + k, n_in, ibal), n);
+      // 4 KiB per step: all loads first, so their latencies overlap
+      for (u32 k0 = 0; k0 < L; k0 += 4096) {
+        u32x4 x[4];
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) {
+          const u32 k = k0 + 1024 * r + lane * 16;
+          x[r] = k < L ? load16_clamped(ib, S + k, n_in, ibal) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) {
+          const u32 k = k0 + 1024 * r + lane * 16;
+          if (k < L) store_exact(ob + op + k, x[r], L - k < 16 ? L - k : 16u);
+        }
       }
       op += L;
       flushed = op;
@@ -421,6 +446,16 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
       wave_lds_fence();
       head += 1;
       pf_head = 0xffffffffu;
+      // the literal's bytes hold no tag starts: resume the bitmap scan at the
+      // word of the next tag instead of scanning the zero words in between
+      if (head == tail) {
+        const u32 nw = (S + L) >> 5;
+        if (nw > scan) {
+          scan = nw;
+          bmw = (lane < kFillWords && scan + lane < nwords) ? bm[scan + lane] : 0u;
+        }
+      }
+      STAMP(7);
       continue;
     }
     const u32 take = bigm ? (u32)__builtin_ctzll(bigm) : take0;
@@ -452,6 +487,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
       pf_cnt = ncnt;
     }
 
+    STAMP(2);
     // ---------- slide the window if this group would overrun it
     if (op + tot_len - sbase > kWindow) {
       const int nsb = (int)(((op - kKeep + obal) & ~15u)) - (int)obal;
@@ -486,6 +522,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     const u32 need_end = kT == 0 ? 0u : (kT == 2 ? At : src + n);
     u8* const wdst = sb + ((int)dst - sbase);
 
+    STAMP(3);
     // ---------- round A: literal pieces and far copies, from global memory
     const bool global_src = has && (kT == 0 || (int)src < sbase);
     if (global_src) {
@@ -496,6 +533,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     }
     wave_lds_fence();
 
+    STAMP(4);
     // ---------- rounds B: near copies, in LDS, in dependency order
     bool done = !has || global_src;
     for (;;) {
@@ -514,12 +552,29 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     op += tot_len;
     head += k_tags;
 
+    STAMP(5);
     // ---------- flush completed 16-byte blocks
     const int fe = (int)((op + obal) & ~15u) - (int)obal;
     if (fe > (int)flushed) flush_to((u32)fe);
+    STAMP(6);
   }
   flush_to(expected);
+#ifdef FSG_STAMPS
+  if (lane == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(&g_stamps[k], (unsigned long long)st_[k]);
+#endif
 }
+
+#ifdef FSG_STAMPS
+extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps));
+  if (reset) {
+    unsigned long long z[16] = {};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
+  }
+  return e == hipSuccess ? 0 : -1;
+}
+#endif
 
 size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;

@@ -208,8 +208,11 @@ void SnappyGpuCodec::Impl::run(const std::vector<Request*>& reqs, bool compress)
     rc = fsg_compress_batch(d_in.as<uint8_t>(), d_in_off, d_in_len, n, max_len, d_out.as<uint8_t>(),
                             d_out_off, d_out_len, d_status, wsp, wsp ? ws : 0, stream);
   } else {
+    // two-pass decoder workspace (tag bitmap); without it the single-pass kernel runs
+    const size_t ws = fsg_decompress_workspace_bytes(n, pos_in);
+    void* wsp = d_ws.reserve(ws) ? d_ws.p : nullptr;
     rc = fsg_decompress_batch(d_in.as<uint8_t>(), d_in_off, d_in_len, n, d_out.as<uint8_t>(), d_out_off,
-                              d_out_cap, d_out_len, d_status, 0, nullptr, 0, stream);
+                              d_out_cap, d_out_len, d_status, 0, wsp, wsp ? ws : 0, stream);
   }
   if (rc != FSG_SUCCESS) {
     fprintf(stderr, "[flare-snappy-gpu] batch launch failed: %s\n", fsg_last_error());

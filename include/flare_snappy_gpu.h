@@ -83,10 +83,13 @@ const char *fsg_last_error(void);
  * 1 = first-generation kernels (decode: one lane per message, tag by tag;
  * encode: one wave per message with the hash table in LDS), 2 = second
  * generation (decode: batched pieces, optional persistent lanes; encode: lane
- * per message, tables in the workspace), 3 = third generation, the default
- * (decode: software-pipelined batched pieces; encode: lane per message with
- * batched speculative probes).  Every variant produces identical bytes and
- * statuses.
+ * per message, tables in the workspace), 3 = third generation (decode:
+ * software-pipelined batched pieces; encode: lane per message with batched
+ * speculative probes, the default encoder), 4 = decode only: the two-pass
+ * decoder (lane-per-message index pass writing a tag-start bitmap, then one
+ * wave per message executing <= 16-byte pieces in dependency rounds through an
+ * LDS output window), the default decoder whenever the workspace holds its
+ * bitmap.  Every variant produces identical bytes and statuses.
  * Process-wide; not for use while other threads launch batches. */
 int fsg_select_kernels(int decode_variant, int encode_variant);
 
@@ -117,10 +120,14 @@ int fsg_uncompressed_lengths_batch(const uint8_t *d_in, const uint64_t *d_in_off
  * max_in_len bounds every message length of the batch (0 = any).  Passing a
  * smaller or NULL workspace selects the LDS-table wave-per-message encoder. */
 size_t fsg_compress_workspace_bytes(uint32_t n_msgs, uint32_t max_in_len);
-/* Device workspace for fsg_decompress_batch: a work counter that lets a
- * bounded number of lanes (fsg_set_decode_lanes) pull messages, which keeps
- * each in-flight message's back-reference window resident in L2/MALL.
- * NULL workspace: one lane per message. */
+/* Device workspace for fsg_decompress_batch.  total_in_bytes = the size of
+ * the packed input (an upper bound of the sum of d_in_len): the two-pass
+ * decoder keeps a tag-start bitmap of 1 bit per input byte there.  With
+ * total_in_bytes = 0 (or a NULL / smaller workspace) the single-pass decoder
+ * runs; a workspace sized for less input than the batch holds still decodes
+ * every message correctly (the overflow falls back to the single-pass
+ * kernel).  The workspace is scratch: its content between calls is
+ * irrelevant. */
 size_t fsg_decompress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_bytes);
 
 /* Batched compress.  Message i is d_in[d_in_off[i] .. +d_in_len[i]); its
