@@ -34,10 +34,12 @@ hipError_t launch_encode_v2(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                             u32* out_len, i32* status, void* ws, size_t ws_bytes,
                             hipStream_t stream);
+size_t encode_plan_bytes(u32 n_msgs, u32 max_in_len);
 hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                             u32* out_len, i32* status, void* ws, size_t ws_bytes,
-                            u32 slots, u32 entries, hipStream_t stream);
+                            u32 slots, u32 entries, size_t tables_bytes, u32 region_cap,
+                            hipStream_t stream);
 hipError_t launch_encode(const u8* in, const u64* in_off, const u32* in_len,
                          u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                          u32* out_len, i32* status, hipStream_t stream);
@@ -58,6 +60,9 @@ std::atomic<int> g_encode_variant{env_int("FSG_ENCODE_KERNEL")};
 // Measured on C3: capping lanes below the message count only removes
 // latency hiding (16384 lanes: 35 ms vs 15 ms with one lane per message).
 std::atomic<unsigned> g_decode_lanes{(unsigned)env_int("FSG_DECODE_LANES")};
+// Test knob: cap the staging region of a split message's fragments (bytes;
+// 0 = slot / fragments).  Small caps force the whole-message fallback pass.
+std::atomic<unsigned> g_region_cap{(unsigned)env_int("FSG_TEST_REGION_CAP")};
 
 int record(hipError_t e, const char* where) {
   if (e == hipSuccess) return FSG_SUCCESS;
@@ -74,6 +79,11 @@ const char* fsg_last_error(void) { return g_err; }
 
 int fsg_set_decode_lanes(uint32_t lanes) {
   g_decode_lanes.store(lanes);
+  return FSG_SUCCESS;
+}
+
+int fsg_set_split_region_cap(uint32_t bytes) {
+  g_region_cap.store(bytes);
   return FSG_SUCCESS;
 }
 
@@ -127,7 +137,9 @@ int fsg_uncompressed_lengths_batch(const uint8_t* d_in, const uint64_t* d_in_off
 }
 
 size_t fsg_compress_workspace_bytes(uint32_t n_msgs, uint32_t max_in_len) {
-  return fsg::encode_v2_workspace_bytes(n_msgs, max_in_len, nullptr);
+  // per-lane hash tables, then the fragment plan for messages > 64 KiB
+  return fsg::encode_v2_workspace_bytes(n_msgs, max_in_len, nullptr) +
+         fsg::encode_plan_bytes(n_msgs, max_in_len);
 }
 size_t fsg_decompress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_bytes) {
   // total_in_bytes = 0: no size known, only the single-pass decoders run.
@@ -157,7 +169,8 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
     if (lanes_cap && lanes_cap < slots) slots = (lanes_cap + 63) / 64 * 64;
     return record(fsg::launch_encode_v3(d_in, d_in_off, d_in_len, n_msgs, max_in_len, d_out,
                                         d_out_off, d_out_len, d_status, d_workspace,
-                                        workspace_bytes, slots, fsg::table_size_for(cap),
+                                        workspace_bytes, slots, fsg::table_size_for(cap), need,
+                                        g_region_cap.load(std::memory_order_relaxed),
                                         (hipStream_t)stream),
                   "fsg_compress_batch");
   }

@@ -111,35 +111,77 @@ __device__ __forceinline__ u8* emit_literal_global(u8* op, const u8* lit, u32 le
 
 }  // namespace
 
+// Work items.  Messages of more than one 64 KiB fragment are split into one
+// item per fragment (fragments compress independently: fresh table, offsets
+// inside the fragment, snappy.cc:875-954), listed by encode_plan_kernel and
+// handed out first; fragment k is staged in region k of the message's slot
+// (R = slot / fragments bytes each) and encode_gather_kernel packs the regions.
+// Then every single-fragment message is one item.  A fragment whose output
+// would not fit its region (only possible for near-incompressible data close
+// to MaxCompressedLength) marks its message kNeedFallback; the fallback pass
+// (FSG_ENC_FALLBACK) re-encodes those messages whole, one lane each.
+constexpr u32 kEncFallback = 1u;
+
 __global__ __launch_bounds__(64) void encode_pipe_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, u8* out,
     const u64* __restrict__ out_off, u32* __restrict__ out_len,
     i32* __restrict__ status, u16* __restrict__ tables, u32 table_entries,
-    u32* __restrict__ work_counter) {
+    u32* __restrict__ ctr, const u32* __restrict__ items, u32* __restrict__ sizes, u32 mode,
+    u32 region_cap) {
   __shared__ u32 win[(kWinDw + 1) * kWave];
   const u32 lane = threadIdx.x;
   const u32 slot = blockIdx.x * blockDim.x + lane;
   u16* table = tables + (u64)slot * table_entries;
   auto wrd = [&](u32 d) -> u32 { return win[d * kWave + lane]; };
+  const bool fallback = mode & kEncFallback;
+  const u32 n_items = (fallback || !items) ? 0u : ctr[1];
 
   for (;;) {
-    const u32 m = atomicAdd(work_counter, 1u);
-    if (m >= n_msgs) break;
+    const u32 w = atomicAdd(&ctr[fallback ? 4 : 0], 1u);
+    u32 m, f_first, f_end;     // message, fragment range [f_first, f_end) in bytes
+    bool staged = false;       // a fragment of a split message
+    if (w < n_items) {
+      m = items[2 * w];
+      f_first = items[2 * w + 1] << kBlockLog;
+      staged = true;
+    } else {
+      m = w - n_items;
+      if (m >= n_msgs) break;
+      if (fallback ? status[m] != kNeedFallback : (items && in_len[m] > kBlockSize)) continue;
+      f_first = 0;
+    }
     const u8* mb = in + in_off[m];
     const u32 total = in_len[m];
+    f_end = staged ? min(total, f_first + kBlockSize) : total;
     u8* const dst = out + out_off[m];
+    const u32 hdr = (u32)varint32_len(total);
     u8* op = dst;
-    {
-      u32 v = total;
-      while (v >= 128) { *op++ = (u8)(v | 128); v >>= 7; }
-      *op++ = (u8)v;
+    u8* op_lim = nullptr;      // staged: last byte a tag may start at (spill room kept)
+    u8* region = dst;
+    if (staged) {
+      const u32 nfr = (total + kBlockSize - 1) >> kBlockLog;
+      u32 R = ((u32)max_compressed_length(total) - hdr) / nfr & ~15u;
+      if (region_cap && region_cap < R) R = region_cap;
+      region = dst + hdr + (u64)(f_first >> kBlockLog) * R;
+      op = region;
+      op_lim = region + R - 32;
     }
+    if (!staged || f_first == 0) {
+      u8* h = dst;
+      u32 v = total;
+      while (v >= 128) { *h++ = (u8)(v | 128); v >>= 7; }
+      *h++ = (u8)v;
+      if (!staged) op = h;
+    }
+    bool ovf = false;
+    // room for `bytes` more output (+16 spill) in a staged region
+    auto room = [&](u32 bytes) -> bool { return !op_lim || op + bytes + 16 <= op_lim; };
     const u32 al = (u32)(reinterpret_cast<uintptr_t>(mb) & 15);
     const u8* abase = mb - al;
     const u32 last_chunk = total ? (al + total - 1) >> 4 : 0u;
 
-    for (u32 fpos = 0; fpos < total; fpos += kBlockSize) {
+    for (u32 fpos = f_first; fpos < f_end && !ovf; fpos += kBlockSize) {
       const u32 n = min(total - fpos, kBlockSize);
       const u8* fb = mb + fpos;
       const u32 ht = table_size_for(n);
@@ -150,6 +192,7 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
         for (u32 i = 0; i < ht / 8; ++i) t4[i] = z;
       }
       if (n < kInputMarginBytes) {  // snappy.cc:346-347,446-450
+        if (!room(n + 5)) { ovf = true; break; }
         op = emit_literal_global(op, fb, n);
         continue;
       }
@@ -285,6 +328,7 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
           for (int k = 1; k < kK; ++k)
             if (win_k == k) { p = P[k]; cand = C[k]; cb = CB[k]; }
           // literal [next_emit, p)
+          if (!room(p - next_emit + 5 + 3 * ((n - p + 63) >> 6) + 3)) { ovf = true; break; }
           if (p > next_emit) {
             const u32 len = p - next_emit;
             if (len <= 16 && in_win(next_emit, 20)) {
@@ -354,25 +398,149 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
           post = false;
         }
       }
-      if (next_emit < n) op = emit_literal_global(op, fb + next_emit, n - next_emit);
+      if (!ovf && next_emit < n) {
+        if (!room(n - next_emit + 5)) { ovf = true; break; }
+        op = emit_literal_global(op, fb + next_emit, n - next_emit);
+      }
     }
-    out_len[m] = (u32)(op - dst);
-    status[m] = kOk;
+    if (staged) {
+      sizes[w] = ovf ? 0xffffffffu : (u32)(op - region);
+    } else {
+      out_len[m] = (u32)(op - dst);
+      status[m] = kOk;
+    }
   }
+}
+
+// Lists the fragments of every message longer than one fragment (one item
+// each) and the messages themselves; ctr[1] = items, ctr[2] = split messages.
+__global__ void encode_plan_kernel(const u32* __restrict__ in_len, u32 n_msgs,
+                                   u32* __restrict__ ctr, u32* __restrict__ items,
+                                   u32* __restrict__ frag_base, u32* __restrict__ big_list) {
+  const u32 m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n_msgs) return;
+  const u32 len = in_len[m];
+  if (len <= kBlockSize) return;
+  const u32 nfr = (len + kBlockSize - 1) >> kBlockLog;
+  const u32 base = atomicAdd(&ctr[1], nfr);
+  frag_base[m] = base;
+  big_list[atomicAdd(&ctr[2], 1u)] = m;
+  for (u32 k = 0; k < nfr; ++k) {
+    items[2 * (base + k)] = m;
+    items[2 * (base + k) + 1] = k;
+  }
+}
+
+// One wave per split message (grid-stride over the list): moves fragments 1..
+// down behind fragment 0
+// (ascending, 4 KiB batches; destinations never pass their sources) and
+// writes the message's length and status.
+__global__ __launch_bounds__(256) void encode_gather_kernel(
+    const u32* __restrict__ in_len, u8* out, const u64* __restrict__ out_off,
+    u32* __restrict__ out_len, i32* __restrict__ status, u32* __restrict__ ctr,
+    const u32* __restrict__ frag_base, const u32* __restrict__ big_list,
+    const u32* __restrict__ sizes, u32 region_cap) {
+  const u32 lane = threadIdx.x & 63;
+  const u32 n_big = ctr[2];
+  const u32 wave0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const u32 n_waves = (gridDim.x * blockDim.x) >> 6;
+  for (u32 idx = wave0; idx < n_big; idx += n_waves) {
+    const u32 m = big_list[idx];
+    const u32 total = in_len[m];
+    const u32 nfr = (total + kBlockSize - 1) >> kBlockLog;
+    const u32 hdr = (u32)varint32_len(total);
+    u32 R = ((u32)max_compressed_length(total) - hdr) / nfr & ~15u;
+    if (region_cap && region_cap < R) R = region_cap;
+    const u32* sz = sizes + frag_base[m];
+    bool bad = false;
+    for (u32 k = lane; k < nfr; k += 64) bad = bad || sz[k] == 0xffffffffu;
+    if (__any(bad)) {
+      if (lane == 0) status[m] = kNeedFallback;
+      continue;
+    }
+    u8* const dst = out + out_off[m];
+    u32 pos = hdr + sz[0];
+    for (u32 k = 1; k < nfr; ++k) {
+      const u8* src = dst + hdr + (u64)k * R;
+      u8* d = dst + pos;
+      const u32 len = sz[k];
+      for (u32 c0 = 0; c0 < len; c0 += 4096) {
+        u32x4 x[4];
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) {
+          const u32 c = c0 + 1024 * r + 16 * lane;
+          if (c < len) __builtin_memcpy(&x[r], src + c, 16);
+        }
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) {
+          const u32 c = c0 + 1024 * r + 16 * lane;
+          if (c < len) {
+            if (c + 16 <= len) {
+              __builtin_memcpy(d + c, &x[r], 16);
+            } else {
+              u8 b[16];
+              __builtin_memcpy(b, &x[r], 16);
+              for (u32 q = 0; q < len - c; ++q) d[c + q] = b[q];
+            }
+          }
+        }
+      }
+      pos += len;
+    }
+    if (lane == 0) {
+      out_len[m] = pos;
+      status[m] = kOk;
+    }
+  }
+}
+
+// Plan region after the tables: items (2 x u32 per fragment), per-item
+// sizes, per-message first item, split-message list.
+size_t encode_plan_bytes(u32 n_msgs, u32 max_in_len) {
+  if (max_in_len <= kBlockSize) return 0;  // (0 = unknown bound: messages are not split)
+  const u64 per_msg = (max_in_len + kBlockSize - 1) >> kBlockLog;
+  const u64 max_items = (u64)n_msgs * per_msg;
+  return (size_t)(max_items * 12 + (u64)n_msgs * 8 + 256);
 }
 
 hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                             u32* out_len, i32* status, void* ws, size_t ws_bytes,
-                            u32 slots, u32 entries, hipStream_t stream) {
+                            u32 slots, u32 entries, size_t tables_bytes, u32 region_cap,
+                            hipStream_t stream) {
   if (n_msgs == 0) return hipSuccess;
-  u32* counter = reinterpret_cast<u32*>(ws);
+  u32* ctr = reinterpret_cast<u32*>(ws);
   u16* tables = reinterpret_cast<u16*>(reinterpret_cast<u8*>(ws) + 256);
-  hipError_t e = hipMemsetAsync(counter, 0, 256, stream);
+  hipError_t e = hipMemsetAsync(ctr, 0, 256, stream);
   if (e != hipSuccess) return e;
+  const size_t plan = encode_plan_bytes(n_msgs, max_in_len);
+  u32 *items = nullptr, *sizes = nullptr, *frag_base = nullptr, *big_list = nullptr;
+  if (plan && ws_bytes >= tables_bytes + plan) {
+    const u64 per_msg = (max_in_len + kBlockSize - 1) >> kBlockLog;
+    const u64 max_items = (u64)n_msgs * per_msg;
+    u8* p = reinterpret_cast<u8*>(ws) + tables_bytes;
+    items = reinterpret_cast<u32*>(p);
+    sizes = items + 2 * max_items;
+    frag_base = sizes + max_items;
+    big_list = frag_base + n_msgs;
+    encode_plan_kernel<<<(n_msgs + 255) / 256, 256, 0, stream>>>(in_len, n_msgs, ctr, items,
+                                                                 frag_base, big_list);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   encode_pipe_kernel<<<slots / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off,
-                                                    out_len, status, tables, entries, counter);
-  return hipGetLastError();
+                                                    out_len, status, tables, entries, ctr, items,
+                                                    sizes, 0u, region_cap);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (items) {
+    encode_gather_kernel<<<1024, 256, 0, stream>>>(in_len, out, out_off, out_len, status, ctr,
+                                                   frag_base, big_list, sizes, region_cap);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    encode_pipe_kernel<<<slots / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off,
+                                                      out_len, status, tables, entries, ctr, nullptr,
+                                                      nullptr, kEncFallback, 0u);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace fsg

@@ -30,6 +30,7 @@ _SIGS = {
     "fsg_last_error": (_c.c_char_p, []),
     "fsg_select_kernels": (_c.c_int, [_c.c_int, _c.c_int]),
     "fsg_set_decode_lanes": (_c.c_int, [_u32]),
+    "fsg_set_split_region_cap": (_c.c_int, [_u32]),
     "fsg_max_compressed_length": (_sz, [_sz]),
     "fsg_get_uncompressed_length": (_c.c_int, [_vp, _sz, _c.POINTER(_u32), _c.c_int]),
     "fsg_uncompressed_lengths_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _c.c_int, _vp]),
@@ -92,6 +93,9 @@ class SnappyGPU:
         import torch
         nbytes = self.lib.fsg_decompress_workspace_bytes(n, total_in)
         return torch.zeros(max(nbytes, 1), dtype=torch.uint8, device=device or f"cuda:{self.device}")
+
+    def set_split_region_cap(self, nbytes: int):
+        self._check(self.lib.fsg_set_split_region_cap(nbytes), "fsg_set_split_region_cap")
 
     def set_decode_lanes(self, lanes: int):
         self._check(self.lib.fsg_set_decode_lanes(lanes), "fsg_set_decode_lanes")

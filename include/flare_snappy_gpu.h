@@ -98,6 +98,13 @@ int fsg_select_kernels(int decode_variant, int encode_variant);
  * bytes are unaffected. */
 int fsg_set_decode_lanes(uint32_t lanes);
 
+/* Test knob: caps the staging region of each fragment of a message longer
+ * than 64 KiB (bytes; 0 = the slot split evenly, the default).  A fragment
+ * whose output does not fit its region sends its message through the
+ * whole-message fallback pass; small caps exercise that path.  Bytes are
+ * unaffected.  Process-wide. */
+int fsg_set_split_region_cap(uint32_t bytes);
+
 /* 32 + n + n/6 (snappy.cc:55-77). */
 size_t fsg_max_compressed_length(size_t n);
 

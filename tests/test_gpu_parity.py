@@ -287,3 +287,27 @@ def test_two_pass_workspace_fallback(gpu, oracle, total_in):
                 assert o == x, i
     finally:
         gpu.codec.select_kernels(0, 0)
+
+
+@pytest.mark.parametrize("cap", [0, 4096, 40000])
+def test_split_message_encode(gpu, oracle, cap):
+    """Messages longer than 64 KiB are encoded one fragment per lane, staged
+    per fragment and packed; capped staging regions force the whole-message
+    fallback pass.  Bytes equal the oracle's either way."""
+    gpu.codec.set_split_region_cap(cap)
+    try:
+        rng = np.random.default_rng(cap + 5)
+        sizes = [65535, 65536, 65537, 131072, 131073, 200000, 1 << 20, 300001, 5, 70000]
+        items = []
+        for i, n in enumerate(sizes):
+            kind = fsg.KIND_RANDOM if i % 3 == 1 else fsg.KIND_TEXT
+            items.append(fsg.make_batch(kind, [n], first_index=100 + i).item(0))
+        items.append(bytes(rng.integers(0, 4, 150000, dtype=np.uint8)))
+        comps, st = gpu.compress(fsg.Batch.from_list(items))
+        assert (st == 0).all()
+        for x, c in zip(items, comps):
+            assert c == oracle.compress(x), len(x)
+        outs, ol, st = gpu.decompress(comps, [len(x) for x in items])
+        assert (st == 0).all() and all(o == x for o, x in zip(outs, items))
+    finally:
+        gpu.codec.set_split_region_cap(0)
