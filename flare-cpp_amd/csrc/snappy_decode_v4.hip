@@ -181,13 +181,15 @@ __global__ __launch_bounds__(64) void index_kernel(
   }
 
   u32 op = 0;
-  // bitmap accumulator: words of the current 128-byte group `cg`
-  u32 acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0, cg = 0;
-  auto flush = [&]() {
-    if (acc0 | acc1 | acc2 | acc3)
-      *reinterpret_cast<u32x4*>(bm + 4 * cg) = u32x4{acc0, acc1, acc2, acc3};
-    acc0 = acc1 = acc2 = acc3 = 0;
-  };
+  // Tag-start bits go to a per-lane LDS ring of 4 groups of 128 input bytes
+  // (group g in slot g & 3, [word][lane]) by a fire-and-forget ds_or; a group
+  // is stored to the bitmap (if it holds bits) once the walk has left it.  One
+  // iteration covers at most 3 groups (the input ring spans 256 bytes, and a
+  // long literal that leaves it ends the lane's iteration).
+  __shared__ u32 bmr[16 * kWave];
+#pragma unroll
+  for (u32 q = 0; q < 16; ++q) bmr[q * kWave + lane] = 0;
+  u32 fg = 0;  // lowest group that may still hold unstored bits
 
   u32x4 g[kAhead];
 #pragma unroll
@@ -200,47 +202,59 @@ __global__ __launch_bounds__(64) void index_kernel(
     // ---------- parse up to kIdxTags tags from the ring
 #pragma unroll
     for (int j = 0; j < kIdxTags; ++j) {
-      const bool need = status < 0;
-      const bool eof = need && ip == n_in;  // RefillTag eof
+      const bool act = status < 0 && ip < n_in;
       const u32 P = ip + ibal;
       const bool inwin = (P + 5 <= 16 * wend) || wend > last_chunk;
       const u32 dw = (P >> 2) & (kRingDwords - 1), bsh = P & 3;
       const u32 lo = ring[dw * kWave + lane], hi = ring[(dw + 1) * kWave + lane];
       const u32 t0 = alignbyte(hi, lo, bsh);     // bytes ip..ip+3
       const u32 b4 = (hi >> (8 * bsh)) & 0xffu;  // byte ip+4
+      // branch-free tag decode (DecompressAllTags :716-787, char_table :516-549):
+      // the 0..4 bytes after the tag byte are a literal's length or a copy's
+      // offset, masked to their count nb
       const u32 c = t0 & 0xffu;
       const u32 type = c & 3;
       const bool is_lit = type == 0;
       const u32 l0 = (c >> 2) + 1;
-      const bool longlit = is_lit && l0 >= 61;   // 1..4 length bytes (:744-750)
-      const u32 nbl = longlit ? l0 - 60 : 0u;
+      const bool longlit = is_lit & (l0 >= 61);  // 1..4 length bytes (:744-750)
+      const u32 nb = is_lit ? (longlit ? l0 - 60 : 0u) : (1u << (type - 1));
       const u32 ext = (b4 << 24) | (t0 >> 8);
-      const u32 msk = nbl >= 4 ? 0xffffffffu : ((1u << (8 * nbl)) - 1u);
-      const u32 litlen = longlit ? (ext & msk) + 1u : l0;  // uint32 wrap: 0xffffffff+1 == 0
-      const u32 nb = is_lit ? nbl : (type == 1 ? 1u : (type == 2 ? 2u : 4u));
-      const u32 clen = type == 1 ? 4 + ((c >> 2) & 7) : l0;
-      const u32 coff = type == 1 ? (((c >> 5) << 8) | ((t0 >> 8) & 0xffu))
-                                 : (type == 2 ? ((t0 >> 8) & 0xffffu) : ext);
-      const u32 len = is_lit ? litlen : clen;
+      const u32 val = nb >= 4 ? ext : ext & ((1u << (8 * nb)) - 1u);
+      const u32 len = is_lit ? (longlit ? val + 1u : l0)  // uint32 wrap: 0xffffffff+1 == 0
+                             : (type == 1 ? 4 + ((c >> 2) & 7) : l0);
+      const u32 coff = type == 1 ? (((c >> 5) << 8) | val) : val;
       const u32 avail = n_in - ip - 1;
-      const u32 space = expected - op;
-      const bool bad = avail < nb ||
-                       (is_lit ? (avail - nb < len || space < len)     // :761, writer overrun
-                               : (coff - 1u >= op || space < len));    // :1200 / :1410,1466
-      const bool hdr = need && !eof && inwin;
-      status = eof ? (op == expected ? kOk : kCorrupt) : ((hdr && bad) ? kCorrupt : status);
-      const bool take = hdr && !bad;
-      if (bm && take) {
-        const u32 gi = ip >> 7;
-        if (gi != cg) { flush(); cg = gi; }
-        const u32 bit = 1u << (ip & 31), wsel = (ip >> 5) & 3;
-        acc0 |= wsel == 0 ? bit : 0u;
-        acc1 |= wsel == 1 ? bit : 0u;
-        acc2 |= wsel == 2 ? bit : 0u;
-        acc3 |= wsel == 3 ? bit : 0u;
-      }
+      const bool bad = (avail < nb) | (expected - op < len) |           // writer overrun
+                       (is_lit ? (avail - nb < len) : (coff - 1u >= op));  // :761 / :1200,1410,1466
+      const bool look = act && inwin;
+      status = (look && bad) ? kCorrupt : status;
+      const bool take = look && !bad;
+      if (bm && take) atomicOr(&bmr[((ip >> 5) & 15) * kWave + lane], 1u << (ip & 31));
       ip = take ? ip + 1 + nb + (is_lit ? len : 0u) : ip;
       op = take ? op + len : op;
+    }
+    // end of input between tags (RefillTag eof): the result, snappy.cc:858-868
+    if (status < 0 && ip == n_in) status = op == expected ? kOk : kCorrupt;
+
+    // ---------- store the bit groups the walk has left
+    if (bm) {
+      const u32 cur = status < 0 ? ip >> 7 : 0xffffffffu;
+#pragma unroll
+      for (u32 k = 0; k < 4; ++k) {
+        const u32 gi = fg + k;
+        if (gi < cur) {
+          const u32 sl = (gi & 3) * 4;
+          u32x4 v;
+#pragma unroll
+          for (u32 q = 0; q < 4; ++q) v[q] = bmr[(sl + q) * kWave + lane];
+          if ((v[0] | v[1] | v[2] | v[3]) && status != kCorrupt) {
+            *reinterpret_cast<u32x4*>(bm + 4 * gi) = v;
+#pragma unroll
+            for (u32 q = 0; q < 4; ++q) bmr[(sl + q) * kWave + lane] = 0;
+          }
+        }
+      }
+      fg = cur > fg + 4 ? cur : (cur > fg ? cur : fg);
     }
 
     // ---------- land the chunks loaded last iteration
@@ -269,7 +283,6 @@ __global__ __launch_bounds__(64) void index_kernel(
     }
     more = __any(status < 0);
   }
-  if (bm && status == kOk) flush();
   if (valid_msg) status_out[m] = status;
 }
 
@@ -306,7 +319,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, u8* out,
     const u64* __restrict__ out_off, const u32* __restrict__ out_len,
-    const i32* __restrict__ status, const u32* __restrict__ bm_base,
+    i32* __restrict__ status, const u32* __restrict__ bm_base,
     const u32* __restrict__ bitmap) {
   __shared__ u32 ring_s[kWavesPerBlock][kTagRing];
   __shared__ u8 pmap_s[kWavesPerBlock][kMaxPieces];
@@ -415,6 +428,10 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
       // ---------- long literal: written straight to the slot by the whole
       // wave; the window restarts behind it
       const u32 L = readlane(len, 0), S = readlane(lsrc, 0);
+      if ((u64)op + L > expected) {  // writer overrun
+        if (lane == 0) status[m] = kCorrupt;
+        return;
+      }
       flush_to(op);
       // 4 KiB per step: all loads first, so their latencies overlap
       for (u32 k0 = 0; k0 < L; k0 += 4096) {
@@ -473,6 +490,13 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     const u32 t_op = op + (incl >> 16) - lv;
     const u32 tot_pc = readlane(incl_pc, k_tags - 1);
     const u32 tot_len = readlane(incl >> 16, k_tags - 1);
+    // copy offset 0 or past the bytes produced so far: the reference's
+    // writer check (snappy.cc:1200, :1410, :1466); the message is corrupt
+    // and the writer's space check (:1166, :1400) against the header length
+    if (__any(v && ((u64)t_op + len > expected || (!is_lit && (coff == 0 || coff > t_op))))) {
+      if (lane == 0) status[m] = kCorrupt;
+      return;
+    }
 
     // ---------- prefetch the next group's tag bytes (lands during this group)
     {
@@ -558,6 +582,10 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     if (fe > (int)flushed) flush_to((u32)fe);
     STAMP(6);
   }
+  if (op != expected) {  // the stream ended early (snappy.cc:858-868)
+    if (lane == 0) status[m] = kCorrupt;
+    return;
+  }
   flush_to(expected);
 #ifdef FSG_STAMPS
   if (lane == 0)
@@ -589,6 +617,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   if (n_msgs == 0) return hipSuccess;
   u8* w = static_cast<u8*>(ws);
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
+  if (ws_bytes < 256 + base_bytes + 4 * 64) return hipErrorInvalidValue;
   u32* counter = reinterpret_cast<u32*>(w);
   u32* bm_base = reinterpret_cast<u32*>(w + 256);
   u32* bitmap = reinterpret_cast<u32*>(w + 256 + base_bytes);
@@ -603,8 +632,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   if ((e = hipGetLastError()) != hipSuccess) return e;
   exec_kernel<<<(n_msgs + kWavesPerBlock - 1) / kWavesPerBlock, kWavesPerBlock * 64, 0, stream>>>(
       in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  return hipSuccess;
+  return hipGetLastError();
 }
 
 }  // namespace fsg
