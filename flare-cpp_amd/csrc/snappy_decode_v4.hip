@@ -313,6 +313,20 @@ __device__ __forceinline__ u32x4 lds_read16(const u8* p) {
   __builtin_memcpy(&v, p, 16);
   return v;
 }
+
+// Inclusive prefix sum over the 64 lanes with DPP row shifts and row
+// broadcasts (gfx9 wave64): 7 VALU steps, no LDS round trip.
+__device__ __forceinline__ u32 dpp_incl_scan(u32 v) {
+  u32 r = v;
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xf, 0xf, true);   // row_shr:3
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x114, 0xf, 0xe, false);  // row_shr:4, banks 1-3
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x118, 0xf, 0xc, false);  // row_shr:8, banks 2-3
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return r;
+}
 }  // namespace
 
 __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
@@ -353,7 +367,12 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
   u32 head = 0, tail = 0, scan = 0, op = 0;
   int sbase = -(int)obal;  // output position of sb[0]
   u32 flushed = 0;         // output [0, flushed) is in global memory
-  u32 bmw = (lane < kFillWords && lane < nwords) ? bm[lane] : 0u;  // next fill, prefetched
+  // next fill, prefetched: lane l holds word scan + l / 4 and takes its byte l % 4
+  auto fill_word = [&](u32 sc) -> u32 {
+    const u32 wi = sc + (lane >> 2);
+    return (lane < 4 * kFillWords && wi < nwords) ? bm[wi] : 0u;
+  };
+  u32 bmw = fill_word(0);
   u32 pf_head = 0xffffffffu, pf_cnt = 0;  // tag bytes prefetched for ring [pf_head, +pf_cnt)
   u32x4 tv = u32x4{0, 0, 0, 0};
 
@@ -378,20 +397,19 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
   for (;;) {
     // ---------- refill the tag ring from the bitmap (keeps >= 64 tags ahead)
     if (tail - head < 2 * kMaxPieces && scan < nwords) {
-      const u32 cnt = __builtin_popcount(bmw);
-      const u32 incl = wave_incl_scan(cnt);
+      u32 bits = (bmw >> (8 * (lane & 3))) & 0xffu;  // 8 bits per lane
+      const u32 cnt = __builtin_popcount(bits);
+      const u32 incl = dpp_incl_scan(cnt);
       u32 slot = tail + incl - cnt;
-      u32 word = bmw;
-      const u32 bitbase = (scan + lane) * 32;
-      while (word) {
-        const u32 b = __builtin_ctz(word);
-        ring[slot & (kTagRing - 1)] = bitbase + b;
+      const u32 bitbase = (scan + (lane >> 2)) * 32 + 8 * (lane & 3);
+      while (bits) {
+        ring[slot & (kTagRing - 1)] = bitbase + __builtin_ctz(bits);
         ++slot;
-        word &= word - 1;
+        bits &= bits - 1;
       }
       tail += readlane(incl, 63);
       scan += kFillWords;
-      bmw = (lane < kFillWords && scan + lane < nwords) ? bm[scan + lane] : 0u;
+      bmw = fill_word(scan);
       wave_lds_fence();
       STAMP(0);
       continue;
@@ -469,7 +487,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
         const u32 nw = (S + L) >> 5;
         if (nw > scan) {
           scan = nw;
-          bmw = (lane < kFillWords && scan + lane < nwords) ? bm[scan + lane] : 0u;
+          bmw = fill_word(scan);
         }
       }
       STAMP(7);
@@ -483,7 +501,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
     const u32 step = pat ? pat_step(coff) : 16u;
     const u32 pc = v ? (pat ? pattern_pieces(len, step) : (len + 15) >> 4) : 0u;
     const u32 lv = v ? len : 0u;
-    const u32 incl = wave_incl_scan(pc | (lv << 16));
+    const u32 incl = dpp_incl_scan(pc | (lv << 16));
     const u32 incl_pc = incl & 0xffffu, excl_pc = incl_pc - pc;
     const bool fits = v && incl_pc <= kMaxPieces;
     const u32 k_tags = (u32)__builtin_popcountll(__ballot(fits));
@@ -598,7 +616,7 @@ extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps));
   if (reset) {
     unsigned long long z[16] = {};
-    hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
   }
   return e == hipSuccess ? 0 : -1;
 }
