@@ -34,8 +34,15 @@ $(LIB)/libflare_rpc_snappy.so: $(HOST_SRC) $(HOST_HDRS) $(LIB)/libflare_snappy_g
 	$(HOSTCXX) -shared -o $@ $(HOST_SRC) -L$(LIB) -lflare_snappy_gpu -L/opt/rocm/lib -lamdhip64 \
 	  -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,/opt/rocm/lib -pthread
 
-# C++ tests mirroring test/rpc/rpc_snappy_compress_test.cc (run by pytest)
-cpptests: build/test_rpc_snappy_compress
+# C++ tests mirroring test/rpc/rpc_snappy_compress_test.cc and the baidu_std /
+# rpc_dump framing (run by pytest)
+cpptests: build/test_rpc_snappy_compress build/test_baidu_std
+
+build/test_baidu_std: tests/cpp/test_baidu_std.cc $(HOST_HDRS) $(LIB)/libflare_rpc_snappy.so
+	@mkdir -p build
+	$(HOSTCXX) -o $@ $< -I$(PKG)/host -L$(LIB) -lflare_rpc_snappy -lflare_snappy_gpu \
+	  -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,$(abspath $(LIB)) -Wl,-rpath,'$$ORIGIN/../$(LIB)' \
+	  -Wl,-rpath,/opt/rocm/lib -pthread
 
 build/test_rpc_snappy_compress: tests/cpp/test_rpc_snappy_compress.cc $(HOST_HDRS) $(LIB)/libflare_rpc_snappy.so
 	@mkdir -p build

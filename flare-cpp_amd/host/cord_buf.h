@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <string>
 #include <string_view>
+#include <utility>
 #include <vector>
 
 namespace flare {
@@ -63,6 +64,12 @@ class cord_buf {
 
   // Remove the first n bytes into `out` (appended), like cutn.
   size_t cutn(cord_buf* out, size_t n);
+  // Drop the first n bytes (cord_buf.h pop_front).
+  size_t pop_front(size_t n) { return cutn(nullptr, n); }
+  void swap(cord_buf& other) noexcept {
+    refs_.swap(other.refs_);
+    std::swap(size_, other.size_);
+  }
 
   bool equals(std::string_view s) const;
 
