@@ -46,6 +46,11 @@ constexpr u32 kRingChunks = 16;              // 16-byte chunks per lane (256 B)
 constexpr u32 kRingDwords = kRingChunks * 4;
 constexpr u32 kAhead = 5;                    // chunks prefetched per iteration
 
+// ---- pass 1b (index_big_kernel) geometry
+constexpr u32 kBigIndexBytes = 48 * 1024;    // compressed sizes above this
+constexpr u32 kBigStageChunks = 5 * 64;      // 16-byte chunks staged per wave
+constexpr u32 kBigStageBytes = 16 * kBigStageChunks;
+
 // ---- pass 2 geometry
 constexpr u32 kWavesPerBlock = 4;
 constexpr u32 kTagRing = 512;                // tag positions per wave (LDS)
@@ -93,6 +98,20 @@ __device__ __forceinline__ u32x4 load16_clamped(const u8* base, u32 off, u32 lim
   return sh ? shr_bytes(v, sh) : v;
 }
 
+// Inclusive prefix sum over the 64 lanes with DPP row shifts and row
+// broadcasts (gfx9 wave64): 7 VALU steps, no LDS round trip.
+__device__ __forceinline__ u32 dpp_incl_scan(u32 v) {
+  u32 r = v;
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xf, 0xf, true);   // row_shr:3
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x114, 0xf, 0xe, false);  // row_shr:4, banks 1-3
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x118, 0xf, 0xc, false);  // row_shr:8, banks 2-3
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return r;
+}
+
 // ceil(len / step) for a pattern copy: len <= 64 and step >= 9 (pat_step of
 // offsets 1..15), so the answer is 1..8 -- counted instead of divided.
 __device__ __forceinline__ u32 pattern_pieces(u32 len, u32 step) {
@@ -112,7 +131,8 @@ __global__ __launch_bounds__(64) void index_kernel(
     const u32* __restrict__ in_len, u32 n_msgs, const u32* __restrict__ out_cap,
     u32* __restrict__ out_len, i32* __restrict__ status_out, u32 flags,
     u32* __restrict__ bm_counter, u32* __restrict__ bm_base_out,
-    u32* __restrict__ bitmap, u64 bm_capacity_words) {
+    u32* __restrict__ bitmap, u64 bm_capacity_words, u32* __restrict__ big_count,
+    u32* __restrict__ big_list) {
   // [dword][lane]; dword 64 = copy of dword 0; 65..68 absorb unused prefetches
   __shared__ u32 ring[(kRingDwords + 5) * kWave];
 
@@ -154,6 +174,22 @@ __global__ __launch_bounds__(64) void index_kernel(
     bm_base = base0 + incl - words;
     if (status < 0 && (u64)bm_base + words > bm_capacity_words) status = kNeedFallback;
     if (valid_msg) bm_base_out[m] = bm_base;
+  }
+
+  // ---- large messages go to index_big_kernel (a whole wave per message);
+  // one lane would walk them serially for tens of milliseconds
+  if (big_list) {
+    const bool big = status < 0 && n_in > kBigIndexBytes;
+    const u64 bb = __ballot(big);
+    if (bb) {
+      u32 base1 = 0;
+      if (lane == 0) base1 = atomicAdd(big_count, (u32)__builtin_popcountll(bb));
+      base1 = readlane(base1, 0);
+      if (big) {
+        big_list[base1 + (u32)__builtin_popcountll(bb & ((1ull << lane) - 1))] = m;
+        status = kNeedBigIndex;
+      }
+    }
   }
   u32* bm = bitmap ? bitmap + bm_base : nullptr;
 
@@ -287,6 +323,138 @@ __global__ __launch_bounds__(64) void index_kernel(
 }
 
 // ===========================================================================
+// Pass 1b: index + validate one LARGE message per wave (compressed size >
+// kBigIndexBytes, listed by pass 1).  One lane walking 100K+ tags serially
+// is the tail of a mixed batch; here the walk advances a 64-byte window
+// [wb, wb+64) at a time: every lane decodes the tag that WOULD start at
+// wb + lane (length, advance, offset, local validity -- the same branch-free
+// decode and checks as pass 1), the real tag starts in the window (the chain
+// from the current position) are found by pointer doubling over the lanes'
+// successor pointers (5 rounds of shuffles), their output positions by a
+// prefix sum, and the position-dependent checks run on all of them at once.
+// Input is staged into LDS 5 KiB at a time.
+// ===========================================================================
+__global__ __launch_bounds__(4 * 64) void index_big_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off,
+    const u32* __restrict__ in_len, const u32* __restrict__ out_len, u32 flags,
+    i32* __restrict__ status_out, const u32* __restrict__ bm_base,
+    u32* __restrict__ bitmap, const u32* __restrict__ big_count,
+    const u32* __restrict__ big_list) {
+  __shared__ u32 stage_s[4][kBigStageBytes / 4 + 4];
+  // wave index made visibly uniform, so the per-message walk state (ip, op,
+  // status, sizes) lives in SGPRs and the walk is scalar code
+  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const u32 lane = threadIdx.x & 63;
+  u32* st = stage_s[wv];
+  const bool strict = flags & 2u;
+  const u32 count = *big_count;
+  const u32 n_waves = gridDim.x * 4;
+
+  for (u32 idx = blockIdx.x * 4 + wv; idx < count; idx += n_waves) {
+    const u32 m = big_list[idx];
+    const u8* ib = in + in_off[m];
+    const u32 n_in = in_len[m];
+    const u32 expected = out_len[m];
+    u32 ulen = 0;
+    u32 ip = (u32)parse_varint_header(ib, n_in, strict, &ulen);  // pass 1 accepted it
+    u32 op = 0;
+    i32 status = -1;
+    u32* bm = bitmap + bm_base[m];
+    const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
+    const u8* abase = ib - ibal;
+    const u32 last_chunk = (ibal + n_in - 1) >> 4;
+    int spos = -1;  // message position of stage byte 0 (-1: nothing staged)
+    u32 send = 0;   // positions [spos, send) are valid in the stage
+
+    while (status < 0) {
+      if (ip >= n_in) {  // end of input between tags (snappy.cc:858-868)
+        status = (ip == n_in && op == expected) ? kOk : kCorrupt;
+        break;
+      }
+      const u32 wb = ip & ~31u;
+      // ---------- stage input covering [wb, wb + 64 + 4)
+      if (spos < 0 || wb < (u32)spos || wb + 72 > send) {
+        const u32 c0 = (wb + ibal) >> 4;
+        u32x4 x[kBigStageChunks / 64];
+#pragma unroll
+        for (u32 r = 0; r < kBigStageChunks / 64; ++r) {
+          u32 k = c0 + r * 64 + lane;
+          k = k <= last_chunk ? k : last_chunk;
+          x[r] = *reinterpret_cast<const u32x4*>(abase + 16 * k);
+        }
+        wave_lds_fence();  // previous window's stage reads are done
+#pragma unroll
+        for (u32 r = 0; r < kBigStageChunks / 64; ++r)
+          *reinterpret_cast<u32x4*>(st + 4 * (r * 64 + lane)) = x[r];
+        wave_lds_fence();
+        spos = (int)(16 * c0) - (int)ibal;
+        send = (u32)spos + kBigStageBytes - 8;
+      }
+      // ---------- every lane decodes the tag that would start at wb + lane
+      const u32 p = wb + lane;
+      const u32 s = p - (u32)spos;
+      const u32 dw = s >> 2, bsh = s & 3;
+      const u32 lo = st[dw], hi = st[dw + 1];
+      const u32 t0 = alignbyte(hi, lo, bsh);
+      const u32 b4 = (hi >> (8 * bsh)) & 0xffu;
+      const u32 c = t0 & 0xffu;
+      const u32 type = c & 3;
+      const bool is_lit = type == 0;
+      const u32 l0 = (c >> 2) + 1;
+      const bool longlit = is_lit & (l0 >= 61);
+      const u32 nb = is_lit ? (longlit ? l0 - 60 : 0u) : (1u << (type - 1));
+      const u32 ext = (b4 << 24) | (t0 >> 8);
+      const u32 val = nb >= 4 ? ext : ext & ((1u << (8 * nb)) - 1u);
+      const u32 len = is_lit ? (longlit ? val + 1u : l0) : (type == 1 ? 4 + ((c >> 2) & 7) : l0);
+      const u32 coff = type == 1 ? (((c >> 5) << 8) | val) : val;
+      const u32 avail = n_in - p - 1;
+      // the checks that need no walk state: tag bytes and literal bytes present
+      const bool bad_local = (p >= n_in) | (avail < nb) | (is_lit & (avail - nb < len));
+      const u32 adv = 1 + nb + (is_lit ? len : 0u);
+      const u32 nxt = p + adv;  // next tag position (meaningful when !bad_local)
+
+      // ---------- which lanes are real tag starts: the chain from ip, by
+      // pointer doubling.  J = successor lane (64 = left the window, or reached
+      // the end of input); after round k, M = the lanes visited within 2^k
+      // steps from this lane.  A 64-byte window holds <= 32 tags (>= 2 bytes
+      // each), so 5 rounds cover any chain.
+      u32 J = (bad_local || adv >= 64 - lane || nxt >= n_in) ? 64u : lane + adv;
+      u64 M = 1ull << lane;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const u32 src = J < 64 ? J : lane;
+        const u64 Mj = ((u64)(u32)__shfl((int)(u32)(M >> 32), (int)src, 64) << 32) |
+                       (u32)__shfl((int)(u32)M, (int)src, 64);
+        const u32 Jj = (u32)__shfl((int)J, (int)src, 64);
+        if (J < 64) {
+          M |= Mj;
+          J = Jj;
+        }
+      }
+      const u32 first = ip - wb;
+      const u64 S = ((u64)readlane((u32)(M >> 32), first) << 32) | readlane((u32)M, first);
+      const bool in_s = (S >> lane) & 1ull;
+      // output position of each chain tag: op + exclusive prefix sum of lengths
+      const u32 lv = in_s ? len : 0u;
+      const u32 t_op = op + dpp_incl_scan(lv) - lv;
+      // writer space and copy offset checks (:761, :1166, :1200, :1410, :1466);
+      // the first failing tag has an exact t_op (every earlier one passed)
+      const bool bad = in_s && (bad_local || expected - t_op < len || (!is_lit && coff - 1u >= t_op));
+      if (__any(bad)) {
+        status = kCorrupt;
+        break;
+      }
+      const u32 last = 63u - (u32)__builtin_clzll(S);
+      ip = readlane(nxt, last);
+      op = readlane(t_op + len, last);
+      const u32 wbits = lane == 0 ? (u32)S : (u32)(S >> 32);
+      if (lane < 2 && wbits) bm[(wb >> 5) + lane] = wbits;
+    }
+    if (lane == 0) status_out[m] = status;
+  }
+}
+
+// ===========================================================================
 // Pass 2: execute.  One wave per status-OK message.
 //
 // Output is assembled in a per-wave LDS window `sb` (kWindow bytes) holding
@@ -314,22 +482,12 @@ __device__ __forceinline__ u32x4 lds_read16(const u8* p) {
   return v;
 }
 
-// Inclusive prefix sum over the 64 lanes with DPP row shifts and row
-// broadcasts (gfx9 wave64): 7 VALU steps, no LDS round trip.
-__device__ __forceinline__ u32 dpp_incl_scan(u32 v) {
-  u32 r = v;
-  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
-  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
-  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xf, 0xf, true);   // row_shr:3
-  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x114, 0xf, 0xe, false);  // row_shr:4, banks 1-3
-  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x118, 0xf, 0xc, false);  // row_shr:8, banks 2-3
-  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x142, 0xa, 0xf, false);  // row_bcast:15
-  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return r;
-}
 }  // namespace
 
-__global__ __launch_bounds__(kWavesPerBlock * 64) void exec_kernel(
+// 6 waves per SIMD (80 VGPRs, LDS 25 KB per block): measured 3% faster than
+// the compiler's 92-VGPR / 5-wave choice on C3; 7 waves (window 3 KiB, spills)
+// and larger windows at 3-4 waves were slower.
+__global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_per_eu(6, 6))) void exec_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, u8* out,
     const u64* __restrict__ out_off, const u32* __restrict__ out_len,
@@ -622,10 +780,12 @@ extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
+// Workspace: [0, 256) counters (bitmap bump allocator at 0, large-message
+// count at 64) | bm_base[n] | big_list[n] | bitmap words.
 size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
   const u64 words = total_in_bytes / 32 + 4ull * n_msgs + 64;
-  return (size_t)(256 + base_bytes + 4 * words);
+  return (size_t)(256 + 2 * base_bytes + 4 * words);
 }
 
 hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
@@ -635,19 +795,30 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   if (n_msgs == 0) return hipSuccess;
   u8* w = static_cast<u8*>(ws);
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
-  if (ws_bytes < 256 + base_bytes + 4 * 64) return hipErrorInvalidValue;
+  if (ws_bytes < 256 + 2 * base_bytes + 4 * 64) return hipErrorInvalidValue;
   u32* counter = reinterpret_cast<u32*>(w);
+  u32* big_count = reinterpret_cast<u32*>(w + 64);
   u32* bm_base = reinterpret_cast<u32*>(w + 256);
-  u32* bitmap = reinterpret_cast<u32*>(w + 256 + base_bytes);
-  const u64 cap_words = (ws_bytes - 256 - base_bytes) / 4;
-  // zero the counter and the bitmap (pass 1 writes only groups holding tags)
-  hipError_t e = hipMemsetAsync(counter, 0, 4, stream);
+  u32* big_list = reinterpret_cast<u32*>(w + 256 + base_bytes);
+  u32* bitmap = reinterpret_cast<u32*>(w + 256 + 2 * base_bytes);
+  const u64 cap_words = (ws_bytes - 256 - 2 * base_bytes) / 4;
+  // zero the counters and the bitmap (pass 1 writes only groups holding tags)
+  hipError_t e = hipMemsetAsync(counter, 0, 256, stream);
   if (e == hipSuccess) e = hipMemsetAsync(bitmap, 0, cap_words * 4, stream);
   if (e != hipSuccess) return e;
   index_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out_cap, out_len,
                                                       status, flags, counter, bm_base, bitmap,
-                                                      cap_words);
+                                                      cap_words, big_count, big_list);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  // large messages: one wave each, 4 per block; waves loop over the list
+  // (its length is only known on the device), so an empty list costs one
+  // short launch
+  {
+    const u32 blocks = n_msgs < 1024 ? (n_msgs + 3) / 4 : 256u;
+    index_big_kernel<<<blocks, 256, 0, stream>>>(in, in_off, in_len, out_len, flags, status,
+                                                 bm_base, bitmap, big_count, big_list);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   exec_kernel<<<(n_msgs + kWavesPerBlock - 1) / kWavesPerBlock, kWavesPerBlock * 64, 0, stream>>>(
       in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap);
   return hipGetLastError();

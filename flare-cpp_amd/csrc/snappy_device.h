@@ -31,6 +31,9 @@ constexpr i32 kSlotTooSmall = 3;
 // fit the workspace); finished by the v3 kernel under kFlagFallbackOnly.
 constexpr i32 kNeedFallback = 0x40000000;
 constexpr u32 kFlagFallbackOnly = 0x80000000u;
+// Internal: a large message left by the lane-per-message index pass for the
+// wave-per-message one (decode v4), which writes its final status.
+constexpr i32 kNeedBigIndex = 0x20000000;
 
 __host__ __device__ inline u64 max_compressed_length(u64 n) {
   return 32 + n + n / 6;  // snappy.cc:55-77

@@ -143,6 +143,40 @@ def test_decode_fuzz_against_oracle(gpu, oracle, variant):
     gpu.codec.select_kernels(0, 0)
 
 
+def test_large_message_index_fuzz(gpu, oracle):
+    """Compressed bodies over 48 KiB take the wave-per-message index pass
+    (index_big_kernel): intact, bit-flipped and truncated ones, mixed with
+    small ones in one batch, against the oracle's verdicts and bytes."""
+    rng = np.random.default_rng(21)
+    srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (120000, 400000, 1 << 20)]
+    srcs.append(fsg.make_batch(fsg.KIND_RANDOM, [70000]).item(0))
+    srcs.append(fsg.make_batch(fsg.KIND_TEXT, [3000]).item(0))  # small, lane path
+    base = [oracle.compress(s) for s in srcs]
+    assert all(len(c) > 48 * 1024 for c in base[:4])
+    comps, caps = [], []
+    for i in range(160):
+        c = bytearray(base[i % len(base)])
+        mode = i // len(base) % 4
+        if mode == 1:
+            for _ in range(int(rng.integers(1, 4))):
+                c[int(rng.integers(len(c)))] = int(rng.integers(256))
+        elif mode == 2:
+            c = c[: int(rng.integers(1, len(c) + 1))]
+        elif mode == 3:  # corrupt late in the stream
+            c[len(c) - 1 - int(rng.integers(min(64, len(c) - 1)))] ^= 0x5A
+        comps.append(bytes(c))
+        caps.append(1 << 21)
+    outs, ol, st = gpu.decompress(comps, caps)
+    for i, (c, o, l, s) in enumerate(zip(comps, outs, ol, st)):
+        ok, ulen, ref = oracle.uncompress(c, cap=1 << 21)
+        if ok is None:
+            assert s == fsg.FSG_SLOT_TOO_SMALL, i
+        elif not ok:
+            assert s in (fsg.FSG_CORRUPT, fsg.FSG_BAD_HEADER), i
+        else:
+            assert s == fsg.FSG_OK and o[:ulen] == ref, i
+
+
 @pytest.mark.parametrize("variant", [1, 2, 3, 4])
 def test_kernel_variants_agree(gpu, oracle, variant):
     """Every generation of kernels gives the oracle's bytes and statuses."""
