@@ -25,10 +25,11 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
-FETCH_SCALE = {"exec_kernel": 2.0, "index_kernel": 2.0}
+FETCH_SCALE = {"exec_kernel": 2.0, "index_kernel": 2.0, "index_big_kernel": 2.0}
 
 OP_KERNELS = {
-    "decompress": ("fsg::index_kernel", "fsg::exec_kernel", "fsg::decode_pipe_kernel"),
+    "decompress": ("fsg::index_kernel", "fsg::index_big_kernel", "fsg::exec_kernel",
+                   "fsg::decode_pipe_kernel"),
     "compress": ("fsg::encode_plan_kernel", "fsg::encode_pipe_kernel", "fsg::encode_gather_kernel"),
 }
 
