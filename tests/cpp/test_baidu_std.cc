@@ -1,5 +1,6 @@
 // test_baidu_std.cc -- baidu_std framing and rpc_dump capture around the GPU
-// snappy handler.
+// snappy handler, and the other protocols' compress-type mappings (SURVEY.md
+// §8(f) rows 2-4).
 //   ./test_baidu_std --cpu                 framing / meta / dump tests (no GPU)
 //   ./test_baidu_std --gpu                 compressed request/response round
 //                                          trips and batch frame decode (MI355X)
@@ -27,7 +28,9 @@
 #include "compress.h"
 #include "cord_buf.h"
 #include "gpu_codec.h"
+#include "protocol_compress.h"
 #include "rpc_dump.h"
+#include "snappy.h"
 #include "snappy_compress.h"
 #include "snappy_message.h"
 
@@ -582,7 +585,79 @@ TEST_CPU(replay_frame_from_sample) {
   ASSERT_EQ(msg.payload.to_string(), "zzzzzzATT");
 }
 
+TEST_CPU(protocol_compress_mappings) {
+  // hulu_pbrpc_protocol.cc:58-98
+  ASSERT_EQ(Hulu2CompressType(HULU_COMPRESS_TYPE_SNAPPY), COMPRESS_TYPE_SNAPPY);
+  ASSERT_EQ(Hulu2CompressType(HULU_COMPRESS_TYPE_ZLIB), COMPRESS_TYPE_ZLIB);
+  ASSERT_EQ(Hulu2CompressType((HuluCompressType)9), COMPRESS_TYPE_NONE);
+  ASSERT_EQ(CompressType2Hulu(COMPRESS_TYPE_SNAPPY), HULU_COMPRESS_TYPE_SNAPPY);
+  ASSERT_EQ(CompressType2Hulu(COMPRESS_TYPE_LZ4), HULU_COMPRESS_TYPE_NONE);
+  // sofa: snappy is 3 on the wire; LZ4 (4) has no mapping back
+  ASSERT_EQ((int)CompressType2Sofa(COMPRESS_TYPE_SNAPPY), 3);
+  ASSERT_EQ(Sofa2CompressType(SOFA_COMPRESS_TYPE_SNAPPY), COMPRESS_TYPE_SNAPPY);
+  ASSERT_EQ(Sofa2CompressType(SOFA_COMPRESS_TYPE_GZIP), COMPRESS_TYPE_GZIP);
+  ASSERT_EQ(Sofa2CompressType(SOFA_COMPRESS_TYPE_LZ4), COMPRESS_TYPE_NONE);
+  ASSERT_EQ(CompressType2Sofa(COMPRESS_TYPE_LZ4), SOFA_COMPRESS_TYPE_NONE);
+  // nova: bit 0 of nshead.version
+  ASSERT_EQ(NovaCompressTypeFromVersion(0x1), COMPRESS_TYPE_SNAPPY);
+  ASSERT_EQ(NovaCompressTypeFromVersion(0x3), COMPRESS_TYPE_SNAPPY);
+  ASSERT_EQ(NovaCompressTypeFromVersion(0x2), COMPRESS_TYPE_NONE);
+  CompressType t = COMPRESS_TYPE_SNAPPY;
+  ASSERT_EQ(NovaResponseVersion(&t), NOVA_SNAPPY_COMPRESS_FLAG);
+  t = COMPRESS_TYPE_GZIP;
+  ASSERT_EQ(NovaResponseVersion(&t), 0);
+  ASSERT_EQ(t, COMPRESS_TYPE_NONE);
+  // public_pbrpc: head compress_type 1 == snappy
+  ASSERT_EQ(PublicPbrpc2CompressType(1), COMPRESS_TYPE_SNAPPY);
+  ASSERT_EQ(PublicPbrpc2CompressType(0), COMPRESS_TYPE_NONE);
+  ASSERT_EQ(PublicPbrpc2CompressType(3), COMPRESS_TYPE_NONE);
+  // request-side support checks
+  SnappyMessageProto req;
+  req.set_text("x");
+  Controller c1;
+  c1.set_request_compress_type(COMPRESS_TYPE_GZIP);
+  cord_buf b;
+  SerializeNovaRequest(&b, &c1, &req);
+  ASSERT_EQ(c1.ErrorCode(), EREQUEST);
+  ASSERT_EQ(c1.ErrorText(), "nova_pbrpc protocol doesn't support compress_type=2");
+  Controller c2;
+  c2.set_request_compress_type(COMPRESS_TYPE_LZ4);
+  SerializePublicPbrpcRequest(&b, &c2, &req);
+  ASSERT_EQ(c2.ErrorText(), "public_pbrpc doesn't support compress type=4");
+  Controller c3;  // NONE passes through to SerializeRequestDefault
+  SerializePublicPbrpcRequest(&b, &c3, &req);
+  ASSERT_FALSE(c3.Failed());
+  ASSERT_EQ(b.to_string(), req.SerializeAsString());
+}
+
 // ---------------------------------------------------------------- GPU tests
+TEST_GPU(nova_and_public_snappy_bodies) {
+  ASSERT_EQ(GlobalInitializeSnappyGpu(), 0);
+  // nova: request compressed because the controller says SNAPPY; the server
+  // reads the flag from nshead.version and parses through the handler
+  SnappyMessageProto req, got;
+  req.set_text(text(5000, 5));
+  req.add_numbers(-1);
+  Controller cc;
+  cc.set_request_compress_type(COMPRESS_TYPE_SNAPPY);
+  cord_buf body;
+  SerializeNovaRequest(&body, &cc, &req);
+  ASSERT_FALSE(cc.Failed());
+  const uint16_t version = NOVA_SNAPPY_COMPRESS_FLAG;
+  ASSERT_TRUE(ParseFromCompressedData(body, &got, NovaCompressTypeFromVersion(version)));
+  ASSERT_EQ(got.SerializeAsString(), req.SerializeAsString());
+  // public_pbrpc: the response string is compressed with the flat API
+  // (public_pbrpc_protocol.cc:137-141) and parsed back by type 1 -> SNAPPY
+  const std::string res = req.SerializeAsString();
+  std::string tmp;
+  flare::snappy::Compress(res.data(), res.size(), &tmp);
+  cord_buf wire;
+  wire.append(tmp);
+  SnappyMessageProto got2;
+  ASSERT_TRUE(ParseFromCompressedData(wire, &got2, PublicPbrpc2CompressType(PUBLIC_PBRPC_COMPRESS_TYPE)));
+  ASSERT_EQ(got2.text(), req.text());
+}
+
 TEST_GPU(snappy_request_response_round_trip) {
   ASSERT_EQ(GlobalInitializeSnappyGpu(), 0);
   for (size_t n : {0ul, 1ul, 200ul, 4093ul, 70000ul, 300000ul}) {
