@@ -725,11 +725,18 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     STAMP(3);
     // ---------- round A: literal pieces and far copies, from global memory
     const bool global_src = has && (kT == 0 || (int)src < sbase);
+    u32x4 xa = u32x4{0, 0, 0, 0};
+    if (global_src)
+      xa = kT == 0 ? load16_clamped(ib, src, n_in, ibal) : load16_clamped(ob, src, expected, obal);
+    // the previous group's completed blocks are flushed while these loads are
+    // in flight (far sources lie before the window: flushed long ago)
+    {
+      const int fe = (int)((op + obal) & ~15u) - (int)obal;
+      if (fe > (int)flushed) flush_to((u32)fe);
+    }
     if (global_src) {
-      u32x4 x = kT == 0 ? load16_clamped(ib, src, n_in, ibal)
-                        : load16_clamped(ob, src, expected, obal);
-      if (kT == 2) x = expand_pattern(x, offT, sel_tab);
-      store_exact(wdst, x, n);
+      if (kT == 2) xa = expand_pattern(xa, offT, sel_tab);
+      store_exact(wdst, xa, n);
     }
     wave_lds_fence();
 
@@ -753,10 +760,6 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     head += k_tags;
 
     STAMP(5);
-    // ---------- flush completed 16-byte blocks
-    const int fe = (int)((op + obal) & ~15u) - (int)obal;
-    if (fe > (int)flushed) flush_to((u32)fe);
-    STAMP(6);
   }
   if (op != expected) {  // the stream ended early (snappy.cc:858-868)
     if (lane == 0) status[m] = kCorrupt;
