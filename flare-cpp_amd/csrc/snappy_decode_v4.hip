@@ -243,31 +243,35 @@ __global__ __launch_bounds__(64) void index_kernel(
       const bool inwin = (P + 5 <= 16 * wend) || wend > last_chunk;
       const u32 dw = (P >> 2) & (kRingDwords - 1), bsh = P & 3;
       const u32 lo = ring[dw * kWave + lane], hi = ring[(dw + 1) * kWave + lane];
-      const u32 t0 = alignbyte(hi, lo, bsh);     // bytes ip..ip+3
-      const u32 b4 = (hi >> (8 * bsh)) & 0xffu;  // byte ip+4
+      const u32 t0 = alignbyte(hi, lo, bsh);          // bytes ip..ip+3
+      const u32 ext = alignbyte(hi >> (8 * bsh), t0, 1);  // bytes ip+1..ip+4
       // branch-free tag decode (DecompressAllTags :716-787, char_table :516-549):
       // the 0..4 bytes after the tag byte are a literal's length or a copy's
-      // offset, masked to their count nb
+      // offset, masked to their count nb.  Written as selects and masks so
+      // the compiler keeps it free of exec-mask branches.
       const u32 c = t0 & 0xffu;
       const u32 type = c & 3;
-      const bool is_lit = type == 0;
       const u32 l0 = (c >> 2) + 1;
-      const bool longlit = is_lit & (l0 >= 61);  // 1..4 length bytes (:744-750)
-      const u32 nb = is_lit ? (longlit ? l0 - 60 : 0u) : (1u << (type - 1));
-      const u32 ext = (b4 << 24) | (t0 >> 8);
-      const u32 val = nb >= 4 ? ext : ext & ((1u << (8 * nb)) - 1u);
-      const u32 len = is_lit ? (longlit ? val + 1u : l0)  // uint32 wrap: 0xffffffff+1 == 0
-                             : (type == 1 ? 4 + ((c >> 2) & 7) : l0);
-      const u32 coff = type == 1 ? (((c >> 5) << 8) | val) : val;
+      const u32 litm = type == 0 ? ~0u : 0u;
+      const u32 nbl = (l0 > 60 ? l0 - 60 : 0u) & litm;        // 1..4 length bytes (:744-750)
+      const u32 nb = ((0x4210u >> (type << 2)) & 0xfu) | nbl;  // copies: 1, 2, 4
+      const u32 val = ext & (0xffffffffu >> ((32 - 8 * nb) & 31));
+      const u32 lc = type == 1 ? 4 + ((c >> 2) & 7) : l0;
+      const u32 len = nbl ? val + 1u : lc;  // uint32 wrap: 0xffffffff+1 == 0
+      const u32 coff = val | ((type == 1 ? c >> 5 : 0u) << 8);
       const u32 avail = n_in - ip - 1;
-      const bool bad = (avail < nb) | (expected - op < len) |           // writer overrun
-                       (is_lit ? (avail - nb < len) : (coff - 1u >= op));  // :761 / :1200,1410,1466
+      // literal bytes present (:761) / copy offset in range (:1200,1410,1466),
+      // merged by mask rather than by a branch
+      const u32 b_lit = (avail - nb < len) ? 1u : 0u;
+      const u32 b_cp = (coff - 1u >= op) ? 1u : 0u;
+      const bool bad = (avail < nb) | (expected - op < len) |  // writer overrun
+                       (((b_lit & litm) | (b_cp & ~litm)) != 0);
       const bool look = act && inwin;
       status = (look && bad) ? kCorrupt : status;
       const bool take = look && !bad;
-      if (bm && take) atomicOr(&bmr[((ip >> 5) & 15) * kWave + lane], 1u << (ip & 31));
-      ip = take ? ip + 1 + nb + (is_lit ? len : 0u) : ip;
-      op = take ? op + len : op;
+      if (bm) atomicOr(&bmr[((ip >> 5) & 15) * kWave + lane], take ? 1u << (ip & 31) : 0u);
+      ip += take ? 1 + nb + (len & litm) : 0u;
+      op += take ? len : 0u;
     }
     // end of input between tags (RefillTag eof): the result, snappy.cc:858-868
     if (status < 0 && ip == n_in) status = op == expected ? kOk : kCorrupt;
