@@ -236,11 +236,16 @@ __global__ __launch_bounds__(64) void index_kernel(
   bool more = __any(status < 0);
   while (more) {
     // ---------- parse up to kIdxTags tags from the ring
+    // a tag at ip is parsed this iteration iff ip < lim: still parsing, before
+    // the end of input, and its 5 bytes are in the ring
+    u32 lim = 0;
+    if (status < 0) {
+      const u32 ring_end = 16 * wend >= 4 + ibal ? 16 * wend - 4 - ibal : 0u;
+      lim = (wend > last_chunk || ring_end > n_in) ? n_in : ring_end;
+    }
 #pragma unroll
     for (int j = 0; j < kIdxTags; ++j) {
-      const bool act = status < 0 && ip < n_in;
       const u32 P = ip + ibal;
-      const bool inwin = (P + 5 <= 16 * wend) || wend > last_chunk;
       const u32 dw = (P >> 2) & (kRingDwords - 1), bsh = P & 3;
       const u32 lo = ring[dw * kWave + lane], hi = ring[(dw + 1) * kWave + lane];
       const u32 t0 = alignbyte(hi, lo, bsh);          // bytes ip..ip+3
@@ -266,8 +271,9 @@ __global__ __launch_bounds__(64) void index_kernel(
       const u32 b_cp = (coff - 1u >= op) ? 1u : 0u;
       const bool bad = (avail < nb) | (expected - op < len) |  // writer overrun
                        (((b_lit & litm) | (b_cp & ~litm)) != 0);
-      const bool look = act && inwin;
+      const bool look = ip < lim;
       status = (look && bad) ? kCorrupt : status;
+      lim = (look && bad) ? 0u : lim;
       const bool take = look && !bad;
       if (bm) atomicOr(&bmr[((ip >> 5) & 15) * kWave + lane], take ? 1u << (ip & 31) : 0u);
       ip += take ? 1 + nb + (len & litm) : 0u;
