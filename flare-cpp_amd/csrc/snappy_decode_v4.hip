@@ -41,10 +41,10 @@ namespace fsg {
 namespace {
 
 // ---- pass 1 geometry (per-lane LDS ring of input chunks, as v3)
-constexpr int kIdxTags = 16;                 // tags per iteration
+constexpr int kIdxTags = 24;                 // tags per iteration
 constexpr u32 kRingChunks = 16;              // 16-byte chunks per lane (256 B)
 constexpr u32 kRingDwords = kRingChunks * 4;
-constexpr u32 kAhead = 5;                    // chunks prefetched per iteration
+constexpr u32 kAhead = 7;                    // chunks prefetched per iteration
 
 // ---- pass 1b (index_big_kernel) geometry
 constexpr u32 kBigIndexBytes = 48 * 1024;    // compressed sizes above this
@@ -511,7 +511,11 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
   if (threadIdx.x < 64) init_pattern_table(sel_tab, threadIdx.x);
   __syncthreads();
 
-  const u32 wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // wave index made visibly uniform: the message's sizes, pointers and the
+  // walk state (head, tail, op, window base) then live in SGPRs and branches
+  // on them are scalar
+  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const u32 lane = threadIdx.x & 63;
   const u32 m = blockIdx.x * kWavesPerBlock + wv;
   if (m >= n_msgs) return;
   if (status[m] != kOk) return;
