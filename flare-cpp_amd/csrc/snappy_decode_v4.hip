@@ -82,11 +82,12 @@ __device__ __forceinline__ u32 readlane(u32 v, u32 l) {
   return (u32)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 
-__device__ __forceinline__ void wave_lds_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+// Orders one wave's LDS accesses across lanes.  A wave's LDS instructions
+// execute in issue order, so a read issued after another lane's write sees
+// it: only the compiler must keep program order (the accesses share one
+// array, so they may alias and are not reordered), and no s_waitcnt is
+// needed -- the wave barrier just pins the schedule.
+__device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_wave_barrier(); }
 
 // 16 bytes of a message buffer at `off`, never touching bytes outside
 // [-(bal), limit) (see clamped_origin).

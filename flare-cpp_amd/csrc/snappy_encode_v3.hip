@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256) void encode_gather_kernel(
     const u32* __restrict__ sizes, u32 region_cap) {
   const u32 lane = threadIdx.x & 63;
   const u32 n_big = ctr[2];
-  const u32 wave0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const u32 wave0 = (u32)__builtin_amdgcn_readfirstlane((int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6));
   const u32 n_waves = (gridDim.x * blockDim.x) >> 6;
   for (u32 idx = wave0; idx < n_big; idx += n_waves) {
     const u32 m = big_list[idx];
