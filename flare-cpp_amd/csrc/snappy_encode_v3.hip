@@ -308,8 +308,13 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
           const u8* a = live[k] ? fb + C[k] : reinterpret_cast<const u8*>(g_enc_dummy);
           __builtin_memcpy(&CB[k], a, 16);
         }
+        // refresh the window from lo_need only once half of it is consumed:
+        // reloading all 80 bytes every batch (text advances ~7 bytes per
+        // batch) cost 5 scattered 16-byte loads per lane per batch
+        const bool pref = (int)lo_need - wbase >= 32;
         u32x4 gn[kWinChunks];
-        const u32 nc = window_chunks(lo_need, gn);
+        u32 nc = 0;
+        if (pref) nc = window_chunks(lo_need, gn);
         // winner
         int win_k = -1;
 #pragma unroll
@@ -388,10 +393,10 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
           ip = p + mlen;
           next_emit = ip;
           post = true;
-          window_store(nc, gn);
+          if (pref) window_store(nc, gn);
           if (ip >= lim) break;  // emit_remainder
         } else {
-          window_store(nc, gn);
+          if (pref) window_store(nc, gn);
           if (stop) break;       // emit_remainder
           ip = s;
           skip = sk;
