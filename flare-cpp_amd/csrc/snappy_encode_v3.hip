@@ -37,9 +37,13 @@ namespace fsg {
 namespace {
 
 #ifndef FSG_V3_PROBES
-#define FSG_V3_PROBES 2
+#define FSG_V3_PROBES 3
 #endif
 constexpr int kK = FSG_V3_PROBES;  // probes per batch
+#ifndef FSG_V3_POST_PROBES
+#define FSG_V3_POST_PROBES 1
+#endif
+constexpr int kPostProbes = FSG_V3_POST_PROBES;  // probes per batch right after a copy
 constexpr u32 kWinChunks = 5;      // 80-byte input window
 constexpr u32 kWinDw = kWinChunks * 4;
 
@@ -249,8 +253,11 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
           }
           const u32 step = sk >> 5;
           const bool bound = s + step <= lim;  // next_ip > ip_limit -> remainder
-          stop = stop || (ok && !bound);
-          ok = ok && bound;
+          // after a copy the next copy usually starts at ip: fewer probes
+          // (a capped probe is simply left for the next batch)
+          const bool capped = post && k >= kPostProbes;
+          stop = stop || (ok && !capped && !bound);
+          ok = ok && bound && !capped;
           P[k] = s;
           live[k] = ok;
           if (ok) { s += step; ++sk; }
