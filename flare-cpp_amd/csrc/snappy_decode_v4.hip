@@ -350,7 +350,7 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
     const u32* __restrict__ in_len, const u32* __restrict__ out_len, u32 flags,
     i32* __restrict__ status_out, const u32* __restrict__ bm_base,
     u32* __restrict__ bitmap, const u32* __restrict__ big_count,
-    const u32* __restrict__ big_list) {
+    const u32* __restrict__ big_list, u32* __restrict__ big_next) {
   __shared__ u32 stage_s[4][kBigStageBytes / 4 + 4];
   // wave index made visibly uniform, so the per-message walk state (ip, op,
   // status, sizes) lives in SGPRs and the walk is scalar code
@@ -359,9 +359,17 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
   u32* st = stage_s[wv];
   const bool strict = flags & 2u;
   const u32 count = *big_count;
-  const u32 n_waves = gridDim.x * 4;
 
-  for (u32 idx = blockIdx.x * 4 + wv; idx < count; idx += n_waves) {
+  // messages are handed out one at a time from a counter: sizes are
+  // power-law distributed, a static stride leaves a few waves with most of
+  // the bytes
+  // (every lane takes part in the atomic, adding 1 for lane 0 and 0 for the
+  // rest, so no lane-0-only branch exists for the compiler to fold the
+  // broadcast into; lane 0's result is the wave's index)
+  for (;;) {
+    const u32 got = atomicAdd(big_next, lane == 0 ? 1u : 0u);
+    const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
+    if (idx >= count) break;
     const u32 m = big_list[idx];
     const u8* ib = in + in_off[m];
     const u32 n_in = in_len[m];
@@ -799,7 +807,7 @@ extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
 #endif
 
 // Workspace: [0, 256) counters (bitmap bump allocator at 0, large-message
-// count at 64) | bm_base[n] | big_list[n] | bitmap words.
+// count at 64, large-message queue head at 128) | bm_base[n] | big_list[n] | bitmap words.
 size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
   const u64 words = total_in_bytes / 32 + 4ull * n_msgs + 64;
@@ -834,7 +842,8 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   {
     const u32 blocks = n_msgs < 1024 ? (n_msgs + 3) / 4 : 256u;
     index_big_kernel<<<blocks, 256, 0, stream>>>(in, in_off, in_len, out_len, flags, status,
-                                                 bm_base, bitmap, big_count, big_list);
+                                                 bm_base, bitmap, big_count, big_list,
+                                                 reinterpret_cast<u32*>(w + 128));
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   exec_kernel<<<(n_msgs + kWavesPerBlock - 1) / kWavesPerBlock, kWavesPerBlock * 64, 0, stream>>>(

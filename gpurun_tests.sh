@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU parity suite + short bench lines, each step under its own time limit.
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 150 python -u -m pytest tests -m gpu -x -v --timeout 60 --timeout-method thread \
   > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -3 gpurun_out/pytest_gpu.log
 for w in ${BENCH_WORKLOADS:-c3-decompress}; do
