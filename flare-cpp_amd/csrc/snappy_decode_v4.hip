@@ -503,30 +503,12 @@ __device__ __forceinline__ u32x4 lds_read16(const u8* p) {
 
 }  // namespace
 
-// 6 waves per SIMD (80 VGPRs, LDS 25 KB per block): measured 3% faster than
-// the compiler's 92-VGPR / 5-wave choice on C3; 7 waves (window 3 KiB, spills)
-// and larger windows at 3-4 waves were slower.
-__global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_per_eu(6, 6))) void exec_kernel(
-    const u8* __restrict__ in, const u64* __restrict__ in_off,
-    const u32* __restrict__ in_len, u32 n_msgs, u8* out,
-    const u64* __restrict__ out_off, const u32* __restrict__ out_len,
-    i32* __restrict__ status, const u32* __restrict__ bm_base,
-    const u32* __restrict__ bitmap) {
-  __shared__ u32 ring_s[kWavesPerBlock][kTagRing];
-  __shared__ u8 pmap_s[kWavesPerBlock][kMaxPieces];
-  __shared__ __attribute__((aligned(16))) u8 sb_s[kWavesPerBlock][kWindow + 32];
-  __shared__ u32x4 sel_tab[16];
-
-  if (threadIdx.x < 64) init_pattern_table(sel_tab, threadIdx.x);
-  __syncthreads();
-
-  // wave index made visibly uniform: the message's sizes, pointers and the
-  // walk state (head, tail, op, window base) then live in SGPRs and branches
-  // on them are scalar
-  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const u32 lane = threadIdx.x & 63;
-  const u32 m = blockIdx.x * kWavesPerBlock + wv;
-  if (m >= n_msgs) return;
+// One message, executed by the calling wave (see the pass-2 comment above).
+__device__ __forceinline__ void exec_message(
+    u32 m, const u8* __restrict__ in, const u64* __restrict__ in_off,
+    const u32* __restrict__ in_len, u8* out, const u64* __restrict__ out_off,
+    const u32* __restrict__ out_len, i32* __restrict__ status, const u32* __restrict__ bm_base,
+    const u32* __restrict__ bitmap, u32* ring, u8* pmap, u8* sb, const u32x4* sel_tab, u32 lane) {
   if (status[m] != kOk) return;
 
   const u32 n_in = in_len[m];
@@ -537,9 +519,6 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
   const u32 obal = (u32)(reinterpret_cast<uintptr_t>(ob) & 15);
   const u32* bm = bitmap + bm_base[m];
   const u32 nwords = (n_in + 31) >> 5;
-  u32* ring = ring_s[wv];
-  u8* pmap = pmap_s[wv];
-  u8* sb = sb_s[wv];
 
 #ifdef FSG_STAMPS
   u64 st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -795,6 +774,54 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
 #endif
 }
 
+// 6 waves per SIMD (62 VGPRs, LDS 25 KB per block); 7 waves (smaller tag ring
+// or window) and larger windows at 3-4 waves were slower.
+// The first kBigBlocks blocks take the large messages listed by pass 1 from a
+// device counter (blocks dispatch in order, so the longest messages start
+// first); every other block runs the wave-per-message mapping and skips them.
+// (A fully persistent grid was measured slower on uniform batches.)
+__global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_per_eu(6, 6))) void exec_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off,
+    const u32* __restrict__ in_len, u32 n_msgs, u8* out,
+    const u64* __restrict__ out_off, const u32* __restrict__ out_len,
+    i32* __restrict__ status, const u32* __restrict__ bm_base,
+    const u32* __restrict__ bitmap, const u32* __restrict__ big_count,
+    const u32* __restrict__ big_list, u32* __restrict__ exec_next, u32 big_blocks) {
+  __shared__ u32 ring_s[kWavesPerBlock][kTagRing];
+  __shared__ u8 pmap_s[kWavesPerBlock][kMaxPieces];
+  __shared__ __attribute__((aligned(16))) u8 sb_s[kWavesPerBlock][kWindow + 32];
+  __shared__ u32x4 sel_tab[16];
+
+  if (threadIdx.x < 64) init_pattern_table(sel_tab, threadIdx.x);
+  __syncthreads();
+
+  // wave index made visibly uniform: the message's sizes, pointers and the
+  // walk state (head, tail, op, window base) then live in SGPRs and branches
+  // on them are scalar
+  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const u32 lane = threadIdx.x & 63;
+  u32* ring = ring_s[wv];
+  u8* pmap = pmap_s[wv];
+  u8* sb = sb_s[wv];
+
+  if (blockIdx.x >= big_blocks) {
+    const u32 m = (blockIdx.x - big_blocks) * kWavesPerBlock + wv;
+    if (m < n_msgs && in_len[m] <= kBigIndexBytes)
+      exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring,
+                   pmap, sb, sel_tab, lane);
+    return;
+  }
+  const u32 nbig = *big_count;
+  if (nbig == 0) return;
+  for (;;) {  // all-lane atomic: lane 0 adds 1, lane 0's result is the index
+    const u32 got = atomicAdd(exec_next, lane == 0 ? 1u : 0u);
+    const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
+    if (idx >= nbig) break;
+    exec_message(big_list[idx], in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap,
+                 ring, pmap, sb, sel_tab, lane);
+  }
+}
+
 #ifdef FSG_STAMPS
 extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps));
@@ -807,7 +834,7 @@ extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
 #endif
 
 // Workspace: [0, 256) counters (bitmap bump allocator at 0, large-message
-// count at 64, large-message queue head at 128) | bm_base[n] | big_list[n] | bitmap words.
+// count at 64, large-message queue heads at 128 and 192) | bm_base[n] | big_list[n] | bitmap words.
 size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
   const u64 words = total_in_bytes / 32 + 4ull * n_msgs + 64;
@@ -846,8 +873,15 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
                                                  reinterpret_cast<u32*>(w + 128));
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  exec_kernel<<<(n_msgs + kWavesPerBlock - 1) / kWavesPerBlock, kWavesPerBlock * 64, 0, stream>>>(
-      in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap);
+  {
+    // large-message blocks (empty when the batch has none: they exit after
+    // one atomic), then one wave per message
+    const u32 small_blocks = (n_msgs + kWavesPerBlock - 1) / kWavesPerBlock;
+    const u32 big_blocks = small_blocks < 256u ? small_blocks : 256u;
+    exec_kernel<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(
+        in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap, big_count,
+        big_list, reinterpret_cast<u32*>(w + 192), big_blocks);
+  }
   return hipGetLastError();
 }
 
