@@ -47,7 +47,8 @@ constexpr u32 kRingDwords = kRingChunks * 4;
 constexpr u32 kAhead = 7;                    // chunks prefetched per iteration
 
 // ---- pass 1b (index_big_kernel) geometry
-constexpr u32 kBigIndexBytes = 48 * 1024;    // compressed sizes above this
+constexpr u32 kBigIndexMin = 8 * 1024;       // large: compressed size above
+constexpr u32 kBigIndexMax = 48 * 1024;      // clamp(4 x the batch mean, min, max)
 constexpr u32 kBigStageChunks = 5 * 64;      // 16-byte chunks staged per wave
 constexpr u32 kBigStageBytes = 16 * kBigStageChunks;
 
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(64) void index_kernel(
     u32* __restrict__ out_len, i32* __restrict__ status_out, u32 flags,
     u32* __restrict__ bm_counter, u32* __restrict__ bm_base_out,
     u32* __restrict__ bitmap, u64 bm_capacity_words, u32* __restrict__ big_count,
-    u32* __restrict__ big_list) {
+    u32* __restrict__ big_list, u32 big_threshold) {
   // [dword][lane]; dword 64 = copy of dword 0; 65..68 absorb unused prefetches
   __shared__ u32 ring[(kRingDwords + 5) * kWave];
 
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(64) void index_kernel(
   // ---- large messages go to index_big_kernel (a whole wave per message);
   // one lane would walk them serially for tens of milliseconds
   if (big_list) {
-    const bool big = status < 0 && n_in > kBigIndexBytes;
+    const bool big = status < 0 && n_in > big_threshold;
     const u64 bb = __ballot(big);
     if (bb) {
       u32 base1 = 0;
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(64) void index_kernel(
 
 // ===========================================================================
 // Pass 1b: index + validate one LARGE message per wave (compressed size >
-// kBigIndexBytes, listed by pass 1).  One lane walking 100K+ tags serially
+// the launch's big_threshold, listed by pass 1).  One lane walking 100K+ tags serially
 // is the tail of a mixed batch; here the walk advances a 64-byte window
 // [wb, wb+64) at a time: every lane decodes the tag that WOULD start at
 // wb + lane (length, advance, offset, local validity -- the same branch-free
@@ -786,7 +787,8 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     const u64* __restrict__ out_off, const u32* __restrict__ out_len,
     i32* __restrict__ status, const u32* __restrict__ bm_base,
     const u32* __restrict__ bitmap, const u32* __restrict__ big_count,
-    const u32* __restrict__ big_list, u32* __restrict__ exec_next, u32 big_blocks) {
+    const u32* __restrict__ big_list, u32* __restrict__ exec_next, u32 big_blocks,
+    u32 big_threshold) {
   __shared__ u32 ring_s[kWavesPerBlock][kTagRing];
   __shared__ u8 pmap_s[kWavesPerBlock][kMaxPieces];
   __shared__ __attribute__((aligned(16))) u8 sb_s[kWavesPerBlock][kWindow + 32];
@@ -806,7 +808,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
 
   if (blockIdx.x >= big_blocks) {
     const u32 m = (blockIdx.x - big_blocks) * kWavesPerBlock + wv;
-    if (m < n_msgs && in_len[m] <= kBigIndexBytes)
+    if (m < n_msgs && in_len[m] <= big_threshold)
       exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring,
                    pmap, sb, sel_tab, lane);
     return;
@@ -859,9 +861,17 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   hipError_t e = hipMemsetAsync(counter, 0, 256, stream);
   if (e == hipSuccess) e = hipMemsetAsync(bitmap, 0, cap_words * 4, stream);
   if (e != hipSuccess) return e;
+  // Large-message threshold: 4x the batch's mean compressed size (estimated
+  // from the workspace, which callers size from the packed input), clamped
+  // to [8, 48] KiB.  The lane pass's time is its longest message; uniform
+  // batches (C2, C3) send nothing to the wave pass.
+  const u64 est_total_in = cap_words > 4ull * n_msgs + 64 ? (cap_words - 4ull * n_msgs - 64) * 32 : 0;
+  u64 thr = 4 * est_total_in / n_msgs;
+  thr = thr < kBigIndexMin ? kBigIndexMin : (thr > kBigIndexMax ? kBigIndexMax : thr);
+  const u32 big_threshold = (u32)thr;
   index_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out_cap, out_len,
                                                       status, flags, counter, bm_base, bitmap,
-                                                      cap_words, big_count, big_list);
+                                                      cap_words, big_count, big_list, big_threshold);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // large messages: one wave each, 4 per block; waves loop over the list
   // (its length is only known on the device), so an empty list costs one
@@ -880,7 +890,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     const u32 big_blocks = small_blocks < 256u ? small_blocks : 256u;
     exec_kernel<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap, big_count,
-        big_list, reinterpret_cast<u32*>(w + 192), big_blocks);
+        big_list, reinterpret_cast<u32*>(w + 192), big_blocks, big_threshold);
   }
   return hipGetLastError();
 }
