@@ -49,6 +49,7 @@ constexpr u32 kAhead = 7;                    // chunks prefetched per iteration
 // ---- pass 1b (index_big_kernel) geometry
 constexpr u32 kBigIndexMin = 8 * 1024;       // large: compressed size above
 constexpr u32 kBigIndexMax = 48 * 1024;      // clamp(4 x the batch mean, min, max)
+constexpr u32 kHugeIndexBytes = 256 * 1024;  // large ones handed out first
 constexpr u32 kBigStageChunks = 5 * 64;      // 16-byte chunks staged per wave
 constexpr u32 kBigStageBytes = 16 * kBigStageChunks;
 
@@ -181,17 +182,25 @@ __global__ __launch_bounds__(64) void index_kernel(
   // ---- large messages go to index_big_kernel (a whole wave per message);
   // one lane would walk them serially for tens of milliseconds
   if (big_list) {
+    // the largest ones (> kHugeIndexBytes) are listed from the end of the
+    // list so both large-message passes hand them out first
     const bool big = status < 0 && n_in > big_threshold;
-    const u64 bb = __ballot(big);
+    const bool huge = big && n_in > kHugeIndexBytes;
+    const u64 bb = __ballot(big && !huge), bh = __ballot(huge);
+    const u64 below = (1ull << lane) - 1;
     if (bb) {
       u32 base1 = 0;
       if (lane == 0) base1 = atomicAdd(big_count, (u32)__builtin_popcountll(bb));
       base1 = readlane(base1, 0);
-      if (big) {
-        big_list[base1 + (u32)__builtin_popcountll(bb & ((1ull << lane) - 1))] = m;
-        status = kNeedBigIndex;
-      }
+      if (big && !huge) big_list[base1 + (u32)__builtin_popcountll(bb & below)] = m;
     }
+    if (bh) {
+      u32 base2 = 0;
+      if (lane == 0) base2 = atomicAdd(big_count + 8, (u32)__builtin_popcountll(bh));
+      base2 = readlane(base2, 0);
+      if (huge) big_list[n_msgs - 1 - (base2 + (u32)__builtin_popcountll(bh & below))] = m;
+    }
+    if (big) status = kNeedBigIndex;
   }
   u32* bm = bitmap ? bitmap + bm_base : nullptr;
 
@@ -351,7 +360,7 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
     const u32* __restrict__ in_len, const u32* __restrict__ out_len, u32 flags,
     i32* __restrict__ status_out, const u32* __restrict__ bm_base,
     u32* __restrict__ bitmap, const u32* __restrict__ big_count,
-    const u32* __restrict__ big_list, u32* __restrict__ big_next) {
+    const u32* __restrict__ big_list, u32* __restrict__ big_next, u32 n_msgs) {
   __shared__ u32 stage_s[4][kBigStageBytes / 4 + 4];
   // wave index made visibly uniform, so the per-message walk state (ip, op,
   // status, sizes) lives in SGPRs and the walk is scalar code
@@ -359,7 +368,8 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
   const u32 lane = threadIdx.x & 63;
   u32* st = stage_s[wv];
   const bool strict = flags & 2u;
-  const u32 count = *big_count;
+  const u32 n_huge = big_count[8];
+  const u32 count = big_count[0] + n_huge;
 
   // messages are handed out one at a time from a counter: sizes are
   // power-law distributed, a static stride leaves a few waves with most of
@@ -371,7 +381,7 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
     const u32 got = atomicAdd(big_next, lane == 0 ? 1u : 0u);
     const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
     if (idx >= count) break;
-    const u32 m = big_list[idx];
+    const u32 m = idx < n_huge ? big_list[n_msgs - 1 - idx] : big_list[idx - n_huge];
     const u8* ib = in + in_off[m];
     const u32 n_in = in_len[m];
     const u32 expected = out_len[m];
@@ -813,14 +823,16 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
                    pmap, sb, sel_tab, lane);
     return;
   }
-  const u32 nbig = *big_count;
+  const u32 n_huge = big_count[8];
+  const u32 nbig = big_count[0] + n_huge;
   if (nbig == 0) return;
   for (;;) {  // all-lane atomic: lane 0 adds 1, lane 0's result is the index
     const u32 got = atomicAdd(exec_next, lane == 0 ? 1u : 0u);
     const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
     if (idx >= nbig) break;
-    exec_message(big_list[idx], in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap,
-                 ring, pmap, sb, sel_tab, lane);
+    const u32 m = idx < n_huge ? big_list[n_msgs - 1 - idx] : big_list[idx - n_huge];
+    exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, pmap,
+                 sb, sel_tab, lane);
   }
 }
 
@@ -836,7 +848,7 @@ extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
 #endif
 
 // Workspace: [0, 256) counters (bitmap bump allocator at 0, large-message
-// count at 64, large-message queue heads at 128 and 192) | bm_base[n] | big_list[n] | bitmap words.
+// count at 64, huge-message count at 96, queue heads at 128 and 192) | bm_base[n] | big_list[n] | bitmap words.
 size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
   const u64 words = total_in_bytes / 32 + 4ull * n_msgs + 64;
@@ -880,7 +892,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     const u32 blocks = n_msgs < 1024 ? (n_msgs + 3) / 4 : 256u;
     index_big_kernel<<<blocks, 256, 0, stream>>>(in, in_off, in_len, out_len, flags, status,
                                                  bm_base, bitmap, big_count, big_list,
-                                                 reinterpret_cast<u32*>(w + 128));
+                                                 reinterpret_cast<u32*>(w + 128), n_msgs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   {
