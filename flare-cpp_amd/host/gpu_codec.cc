@@ -68,16 +68,23 @@ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 }  // namespace
 
+// A large batch is cut into chunks of consecutive messages (>= kChunkBytes of
+// input each, at most kSlots in flight): chunk k's gather into pinned staging
+// runs on the CPU while chunk k-1's H2D / kernels / D2H run on the GPU, and
+// chunks on different streams overlap their copies with each other's kernels.
+constexpr int kSlots = 3;
+
 struct SnappyGpuCodec::Impl {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t streams[kSlots] = {};
+  size_t chunk_bytes = 64ull << 20;  // FLARE_SNAPPY_GPU_CHUNK_BYTES
 
   std::mutex mu;
   std::condition_variable cv;
   std::deque<Request*> queue;
   bool busy = false;
 
-  DevBuf d_in, d_meta, d_out, d_ws;
+  DevBuf d_in, d_meta, d_out, d_ws[kSlots];
   HostBuf h_in, h_meta, h_out;
   CodecStats stats;
 
@@ -97,15 +104,20 @@ SnappyGpuCodec::SnappyGpuCodec() : impl_(new Impl) {
     err_ = std::string("fsg_init failed: ") + fsg_last_error();
     return;
   }
-  if (hipStreamCreateWithFlags(&impl_->stream, hipStreamNonBlocking) != hipSuccess) {
-    err_ = "hipStreamCreate failed";
-    return;
+  for (auto& st : impl_->streams) {
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+      err_ = "hipStreamCreate failed";
+      return;
+    }
   }
+  if (const char* cb = getenv("FLARE_SNAPPY_GPU_CHUNK_BYTES")) impl_->chunk_bytes = strtoull(cb, nullptr, 10);
+  if (impl_->chunk_bytes == 0) impl_->chunk_bytes = 1;
   ok_ = true;
 }
 
 SnappyGpuCodec::~SnappyGpuCodec() {
-  if (impl_->stream) (void)hipStreamDestroy(impl_->stream);
+  for (auto& st : impl_->streams)
+    if (st) (void)hipStreamDestroy(st);
   delete impl_;
 }
 
@@ -164,8 +176,17 @@ void SnappyGpuCodec::Impl::run(const std::vector<Request*>& reqs, bool compress)
   auto* out_cap = reinterpret_cast<uint32_t*>(m + 20ull * n);
   auto* out_len = reinterpret_cast<uint32_t*>(m + 24ull * n);
   auto* status = reinterpret_cast<int32_t*>(m + 28ull * n);
-  // ---- gather: cord_buf backing blocks -> pinned staging (cord_buf.cc:1469-1475)
+  uint8_t* dm = d_meta.as<uint8_t>();
+  auto* d_in_off = reinterpret_cast<uint64_t*>(dm);
+  auto* d_out_off = reinterpret_cast<uint64_t*>(dm + 8ull * n);
+  auto* d_in_len = reinterpret_cast<uint32_t*>(dm + 16ull * n);
+  auto* d_out_cap = reinterpret_cast<uint32_t*>(dm + 20ull * n);
+  auto* d_out_len = reinterpret_cast<uint32_t*>(dm + 24ull * n);
+  auto* d_status = reinterpret_cast<int32_t*>(dm + 28ull * n);
   uint8_t* hin = h_in.as<uint8_t>();
+  const uint8_t* hout = h_out.as<uint8_t>();
+
+  // ---- layout (offsets only; the copies happen per chunk)
   size_t pos_in = 0, pos_out = 0;
   for (uint32_t i = 0; i < n; ++i) {
     in_off[i] = pos_in;
@@ -175,68 +196,118 @@ void SnappyGpuCodec::Impl::run(const std::vector<Request*>& reqs, bool compress)
       out_cap[i] = 0;
       continue;
     }
-    const cord_buf& in = *reqs[i]->in;
-    size_t w = 0;
-    for (size_t b = 0; b < in.backing_block_num(); ++b) {
-      std::string_view blk = in.backing_block(b);
-      memcpy(hin + pos_in + w, blk.data(), blk.size());
-      w += blk.size();
-    }
+    const size_t w = reqs[i]->in->size();
     in_len[i] = (uint32_t)w;
     pos_in += align16(w);
     const size_t cap = compress ? fsg_max_compressed_length(w) : ulen[i];
     out_cap[i] = (uint32_t)cap;
     pos_out += align16(cap);
   }
-  // ---- H2D, kernels, D2H on one stream
-  uint8_t* dm = d_meta.as<uint8_t>();
-  if (hipMemcpyAsync(d_in.p, hin, pos_in ? pos_in : 1, hipMemcpyHostToDevice, stream) != hipSuccess ||
-      hipMemcpyAsync(dm, m, 24ull * n, hipMemcpyHostToDevice, stream) != hipSuccess) {  // offsets, lens, caps
-    fprintf(stderr, "[flare-snappy-gpu] H2D copy failed\n");
-    return;
-  }
-  auto* d_in_off = reinterpret_cast<uint64_t*>(dm);
-  auto* d_out_off = reinterpret_cast<uint64_t*>(dm + 8ull * n);
-  auto* d_in_len = reinterpret_cast<uint32_t*>(dm + 16ull * n);
-  auto* d_out_cap = reinterpret_cast<uint32_t*>(dm + 20ull * n);
-  auto* d_out_len = reinterpret_cast<uint32_t*>(dm + 24ull * n);
-  auto* d_status = reinterpret_cast<int32_t*>(dm + 28ull * n);
-  int rc;
-  if (compress) {
-    const size_t ws = fsg_compress_workspace_bytes(n, max_len);
-    void* wsp = d_ws.reserve(ws) ? d_ws.p : nullptr;  // no workspace -> LDS-table kernel
-    rc = fsg_compress_batch(d_in.as<uint8_t>(), d_in_off, d_in_len, n, max_len, d_out.as<uint8_t>(),
-                            d_out_off, d_out_len, d_status, wsp, wsp ? ws : 0, stream);
-  } else {
-    // two-pass decoder workspace (tag bitmap); without it the single-pass kernel runs
-    const size_t ws = fsg_decompress_workspace_bytes(n, pos_in);
-    void* wsp = d_ws.reserve(ws) ? d_ws.p : nullptr;
-    rc = fsg_decompress_batch(d_in.as<uint8_t>(), d_in_off, d_in_len, n, d_out.as<uint8_t>(), d_out_off,
-                              d_out_cap, d_out_len, d_status, 0, wsp, wsp ? ws : 0, stream);
-  }
-  if (rc != FSG_SUCCESS) {
-    fprintf(stderr, "[flare-snappy-gpu] batch launch failed: %s\n", fsg_last_error());
-    return;
-  }
-  if (hipMemcpyAsync(m + 24ull * n, d_out_len, 8ull * n, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-      hipMemcpyAsync(h_out.p, d_out.p, pos_out ? pos_out : 1, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-      hipStreamSynchronize(stream) != hipSuccess) {
-    fprintf(stderr, "[flare-snappy-gpu] stream error\n");
-    return;
-  }
-  // ---- scatter: append results to the callers' cord_bufs
-  const uint8_t* hout = h_out.as<uint8_t>();
+  // ---- chunks: [first, end) message ranges of >= chunk_bytes input
+  std::vector<uint32_t> cut{0};
+  for (uint32_t i = 0; i < n; ++i)
+    if (i + 1 < n && in_off[i + 1] - in_off[cut.back()] >= chunk_bytes) cut.push_back(i + 1);
+  cut.push_back(n);
+  const size_t n_chunks = cut.size() - 1;
+
+  bool failed = false;
+  std::vector<int> pending(kSlots, -1);  // chunk in flight on each stream
   uint64_t bytes_out = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    Request* r = reqs[i];
-    if (skip[i] || status[i] != FSG_OK) {
-      r->ok = false;
-      continue;
+  auto finish = [&](int slot) {  // wait for a slot's chunk, scatter its results
+    const int k = pending[slot];
+    if (k < 0) return;
+    pending[slot] = -1;
+    if (hipStreamSynchronize(streams[slot]) != hipSuccess) {
+      fprintf(stderr, "[flare-snappy-gpu] stream error\n");
+      failed = true;
+      return;
     }
-    r->out->append(hout + out_off[i], out_len[i]);
-    r->ok = true;
-    bytes_out += out_len[i];
+    // ---- scatter: append results to the callers' cord_bufs
+    for (uint32_t i = cut[k]; i < cut[k + 1]; ++i) {
+      Request* r = reqs[i];
+      if (skip[i] || status[i] != FSG_OK) {
+        r->ok = false;
+        continue;
+      }
+      r->out->append(hout + out_off[i], out_len[i]);
+      r->ok = true;
+      bytes_out += out_len[i];
+    }
+  };
+  for (size_t k = 0; k < n_chunks && !failed; ++k) {
+    const int slot = (int)(k % kSlots);
+    finish(slot);  // its previous chunk (staging regions are disjoint, streams are not)
+    if (failed) break;
+    const uint32_t a = cut[k], b = cut[k + 1], cn = b - a;
+    // ---- gather: cord_buf backing blocks -> pinned staging (cord_buf.cc:1469-1475)
+    for (uint32_t i = a; i < b; ++i) {
+      if (skip[i]) continue;
+      const cord_buf& in = *reqs[i]->in;
+      size_t w = 0;
+      for (size_t blk = 0; blk < in.backing_block_num(); ++blk) {
+        std::string_view v = in.backing_block(blk);
+        memcpy(hin + in_off[i] + w, v.data(), v.size());
+        w += v.size();
+      }
+    }
+    hipStream_t st = streams[slot];
+    const size_t ia = in_off[a], ib = b < n ? in_off[b] : pos_in;
+    const size_t oa = out_off[a], ob = b < n ? out_off[b] : pos_out;
+    bool ok = true;
+    ok = ok && (ib == ia || hipMemcpyAsync(d_in.as<uint8_t>() + ia, hin + ia, ib - ia,
+                                           hipMemcpyHostToDevice, st) == hipSuccess);
+    // this chunk's offsets, lengths and caps (four column slices)
+    ok = ok && hipMemcpyAsync(d_in_off + a, in_off + a, 8ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
+    ok = ok && hipMemcpyAsync(d_out_off + a, out_off + a, 8ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
+    ok = ok && hipMemcpyAsync(d_in_len + a, in_len + a, 4ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
+    ok = ok && hipMemcpyAsync(d_out_cap + a, out_cap + a, 4ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
+    if (!ok) {
+      fprintf(stderr, "[flare-snappy-gpu] H2D copy failed\n");
+      failed = true;
+      break;
+    }
+    int rc;
+    if (compress) {
+      uint32_t cmax = 0;
+      for (uint32_t i = a; i < b; ++i) cmax = std::max(cmax, in_len[i]);
+      const size_t ws = fsg_compress_workspace_bytes(cn, cmax);
+      void* wsp = d_ws[slot].reserve(ws) ? d_ws[slot].p : nullptr;  // no workspace -> LDS-table kernel
+      rc = fsg_compress_batch(d_in.as<uint8_t>(), d_in_off + a, d_in_len + a, cn, cmax,
+                              d_out.as<uint8_t>(), d_out_off + a, d_out_len + a, d_status + a, wsp,
+                              wsp ? ws : 0, st);
+    } else {
+      // two-pass decoder workspace (tag bitmap); without it the single-pass kernel runs
+      const size_t ws = fsg_decompress_workspace_bytes(cn, ib - ia);
+      void* wsp = d_ws[slot].reserve(ws) ? d_ws[slot].p : nullptr;
+      rc = fsg_decompress_batch(d_in.as<uint8_t>(), d_in_off + a, d_in_len + a, cn, d_out.as<uint8_t>(),
+                                d_out_off + a, d_out_cap + a, d_out_len + a, d_status + a, 0, wsp,
+                                wsp ? ws : 0, st);
+    }
+    if (rc != FSG_SUCCESS) {
+      fprintf(stderr, "[flare-snappy-gpu] batch launch failed: %s\n", fsg_last_error());
+      failed = true;
+      break;
+    }
+    ok = hipMemcpyAsync(out_len + a, d_out_len + a, 4ull * cn, hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipMemcpyAsync(status + a, d_status + a, 4ull * cn, hipMemcpyDeviceToHost, st) == hipSuccess &&
+         (ob == oa || hipMemcpyAsync(h_out.as<uint8_t>() + oa, d_out.as<uint8_t>() + oa, ob - oa,
+                                     hipMemcpyDeviceToHost, st) == hipSuccess);
+    if (!ok) {
+      fprintf(stderr, "[flare-snappy-gpu] D2H copy failed\n");
+      failed = true;
+      break;
+    }
+    pending[slot] = (int)k;
   }
+  for (int s2 = 0; s2 < kSlots; ++s2) {  // drain (results of a failed batch stay !ok)
+    if (failed) {
+      if (pending[s2] >= 0) (void)hipStreamSynchronize(streams[s2]);
+      pending[s2] = -1;
+    } else {
+      finish(s2);
+    }
+  }
+  if (failed) return;  // requests of unfinished chunks stay !ok
   std::lock_guard<std::mutex> lk(mu);
   stats.batches += 1;
   stats.messages += n;

@@ -16,6 +16,7 @@ The C++ binary's own --cpu cases (header bytes, parse errors, attachment
 split, dump files) run here too; --gpu cases run on the MI355X.
 """
 import json
+import os
 import struct
 import subprocess
 from pathlib import Path
@@ -254,8 +255,12 @@ def test_framing_cpu_cases():
 
 
 @pytest.mark.gpu
-def test_framing_gpu_cases():
-    r = subprocess.run([str(_binary()), "--gpu"], capture_output=True, text=True, timeout=600)
+@pytest.mark.parametrize("chunk_bytes", [None, "4096"])
+def test_framing_gpu_cases(chunk_bytes):
+    env = dict(os.environ)
+    if chunk_bytes:  # many chunks: the host runtime's multi-stream pipeline
+        env["FLARE_SNAPPY_GPU_CHUNK_BYTES"] = chunk_bytes
+    r = subprocess.run([str(_binary()), "--gpu"], capture_output=True, text=True, timeout=600, env=env)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert " 0 failures" in r.stdout

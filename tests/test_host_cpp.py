@@ -2,6 +2,7 @@
 policy::SnappyCompress/SnappyDecompress, flat flare::snappy API, cross-call
 batcher), exercised by tests/cpp/test_rpc_snappy_compress.cc -- the reference's
 rpc_snappy_compress_test.cc cases re-run against the GPU handler."""
+import os
 import subprocess
 from pathlib import Path
 
@@ -24,8 +25,14 @@ def test_host_layer_cpu_cases():
 
 
 @pytest.mark.gpu
-def test_host_layer_gpu_cases():
-    r = subprocess.run([str(_binary()), "--gpu"], capture_output=True, text=True, timeout=600)
+@pytest.mark.parametrize("chunk_bytes", [None, "4096"])
+def test_host_layer_gpu_cases(chunk_bytes):
+    """chunk_bytes 4096 cuts every batch into many chunks, so the host runtime's
+    pipeline (gather / H2D / kernels / D2H / scatter over three streams) runs."""
+    env = dict(os.environ)
+    if chunk_bytes:
+        env["FLARE_SNAPPY_GPU_CHUNK_BYTES"] = chunk_bytes
+    r = subprocess.run([str(_binary()), "--gpu"], capture_output=True, text=True, timeout=600, env=env)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failures" in r.stdout
