@@ -3,12 +3,15 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
+#include <thread>
+#include <vector>
 
 #include "../../include/flare_snappy_gpu.h"
 
@@ -66,6 +69,37 @@ struct Request {
 
 inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
+// Host threads for gather / scatter of large chunks (the copies into and out
+// of pinned staging are CPU memcpy; one core moves ~10 GB/s).
+unsigned host_threads() {
+  static const unsigned t = [] {
+    if (const char* e = getenv("FLARE_SNAPPY_GPU_HOST_THREADS")) return (unsigned)std::max(1, atoi(e));
+    const unsigned hw = std::thread::hardware_concurrency();
+    return std::min(16u, std::max(1u, hw));
+  }();
+  return t;
+}
+
+// fn(i) for i in [a, b), split over host threads when `bytes` is large.
+template <class F>
+void parallel_for(uint32_t a, uint32_t b, size_t bytes, F&& fn) {
+  const unsigned nt = bytes < (8u << 20) ? 1u : std::min<unsigned>(host_threads(), b - a);
+  if (nt <= 1) {
+    for (uint32_t i = a; i < b; ++i) fn(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (unsigned t = 0; t < nt; ++t) {
+    const uint32_t lo = a + (uint32_t)((uint64_t)(b - a) * t / nt);
+    const uint32_t hi = a + (uint32_t)((uint64_t)(b - a) * (t + 1) / nt);
+    th.emplace_back([lo, hi, &fn] {
+      for (uint32_t i = lo; i < hi; ++i) fn(i);
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
 }  // namespace
 
 // A large batch is cut into chunks of consecutive messages (>= kChunkBytes of
@@ -77,7 +111,12 @@ constexpr int kSlots = 3;
 struct SnappyGpuCodec::Impl {
   int device = 0;
   hipStream_t streams[kSlots] = {};
-  size_t chunk_bytes = 64ull << 20;  // FLARE_SNAPPY_GPU_CHUNK_BYTES
+  // Decode is copy-bound end to end and pipelines well in 256 MiB chunks;
+  // encode is latency-bound on the GPU and needs every message of the batch
+  // in one launch, so it is not chunked.  FLARE_SNAPPY_GPU_CHUNK_BYTES
+  // overrides both (tests force many small chunks).
+  size_t chunk_bytes = 256ull << 20;
+  size_t chunk_bytes_compress = ~size_t(0);
 
   std::mutex mu;
   std::condition_variable cv;
@@ -110,8 +149,10 @@ SnappyGpuCodec::SnappyGpuCodec() : impl_(new Impl) {
       return;
     }
   }
-  if (const char* cb = getenv("FLARE_SNAPPY_GPU_CHUNK_BYTES")) impl_->chunk_bytes = strtoull(cb, nullptr, 10);
-  if (impl_->chunk_bytes == 0) impl_->chunk_bytes = 1;
+  if (const char* cb = getenv("FLARE_SNAPPY_GPU_CHUNK_BYTES")) {
+    impl_->chunk_bytes = std::max<size_t>(1, strtoull(cb, nullptr, 10));
+    impl_->chunk_bytes_compress = impl_->chunk_bytes;
+  }
   ok_ = true;
 }
 
@@ -205,8 +246,9 @@ void SnappyGpuCodec::Impl::run(const std::vector<Request*>& reqs, bool compress)
   }
   // ---- chunks: [first, end) message ranges of >= chunk_bytes input
   std::vector<uint32_t> cut{0};
+  const size_t cbytes = compress ? chunk_bytes_compress : chunk_bytes;
   for (uint32_t i = 0; i < n; ++i)
-    if (i + 1 < n && in_off[i + 1] - in_off[cut.back()] >= chunk_bytes) cut.push_back(i + 1);
+    if (i + 1 < n && in_off[i + 1] - in_off[cut.back()] >= cbytes) cut.push_back(i + 1);
   cut.push_back(n);
   const size_t n_chunks = cut.size() - 1;
 
@@ -222,7 +264,9 @@ void SnappyGpuCodec::Impl::run(const std::vector<Request*>& reqs, bool compress)
       failed = true;
       return;
     }
-    // ---- scatter: append results to the callers' cord_bufs
+    // ---- scatter: append results to the callers' cord_bufs.  Serial: the
+    // appends allocate fresh blocks, and page faults from many threads at once
+    // measured 3x slower than one thread.
     for (uint32_t i = cut[k]; i < cut[k + 1]; ++i) {
       Request* r = reqs[i];
       if (skip[i] || status[i] != FSG_OK) {
@@ -240,8 +284,9 @@ void SnappyGpuCodec::Impl::run(const std::vector<Request*>& reqs, bool compress)
     if (failed) break;
     const uint32_t a = cut[k], b = cut[k + 1], cn = b - a;
     // ---- gather: cord_buf backing blocks -> pinned staging (cord_buf.cc:1469-1475)
-    for (uint32_t i = a; i < b; ++i) {
-      if (skip[i]) continue;
+    const size_t ia = in_off[a], ib = b < n ? in_off[b] : pos_in;
+    parallel_for(a, b, ib - ia, [&](uint32_t i) {
+      if (skip[i]) return;
       const cord_buf& in = *reqs[i]->in;
       size_t w = 0;
       for (size_t blk = 0; blk < in.backing_block_num(); ++blk) {
@@ -249,9 +294,8 @@ void SnappyGpuCodec::Impl::run(const std::vector<Request*>& reqs, bool compress)
         memcpy(hin + in_off[i] + w, v.data(), v.size());
         w += v.size();
       }
-    }
+    });
     hipStream_t st = streams[slot];
-    const size_t ia = in_off[a], ib = b < n ? in_off[b] : pos_in;
     const size_t oa = out_off[a], ob = b < n ? out_off[b] : pos_out;
     bool ok = true;
     ok = ok && (ib == ia || hipMemcpyAsync(d_in.as<uint8_t>() + ia, hin + ia, ib - ia,
