@@ -254,11 +254,20 @@ __global__ __launch_bounds__(64) void index_kernel(
       const u32 ring_end = 16 * wend >= 4 + ibal ? 16 * wend - 4 - ibal : 0u;
       lim = (wend > last_chunk || ring_end > n_in) ? n_in : ring_end;
     }
+    // Software-pipelined: tag j+1's ring read is issued (in program order)
+    // before tag j's checks and its ds_or, so the LDS latency overlaps them;
+    // the compiler does not move LDS reads above the atomic.
+    auto ring_read = [&](u32 at, u32& lo, u32& hi) {
+      const u32 P = at + ibal;
+      const u32 dw = (P >> 2) & (kRingDwords - 1);
+      lo = ring[dw * kWave + lane];
+      hi = ring[(dw + 1) * kWave + lane];
+    };
+    u32 lo, hi;
+    ring_read(ip, lo, hi);
 #pragma unroll
     for (int j = 0; j < kIdxTags; ++j) {
-      const u32 P = ip + ibal;
-      const u32 dw = (P >> 2) & (kRingDwords - 1), bsh = P & 3;
-      const u32 lo = ring[dw * kWave + lane], hi = ring[(dw + 1) * kWave + lane];
+      const u32 bsh = (ip + ibal) & 3;
       const u32 t0 = alignbyte(hi, lo, bsh);          // bytes ip..ip+3
       const u32 ext = alignbyte(hi >> (8 * bsh), t0, 1);  // bytes ip+1..ip+4
       // branch-free tag decode (DecompressAllTags :716-787, char_table :516-549):
@@ -274,6 +283,14 @@ __global__ __launch_bounds__(64) void index_kernel(
       const u32 val = ext & (0xffffffffu >> ((32 - 8 * nb) & 31));
       const u32 lc = type == 1 ? 4 + ((c >> 2) & 7) : l0;
       const u32 len = nbl ? val + 1u : lc;  // uint32 wrap: 0xffffffff+1 == 0
+      // The walk advances over every tag below lim whether or not it passed
+      // its checks, so the checks stay off the ip -> ip dependency chain.
+      // After the first failing tag the status is final (kCorrupt): what the
+      // walk reads from there on only sets bits in the LDS ring, which are
+      // never stored for a corrupt message, and ring indices are masked.
+      const bool look = ip < lim;
+      const u32 ip_next = ip + (look ? 1 + nb + (len & litm) : 0u);
+      if (j + 1 < kIdxTags) ring_read(ip_next, lo, hi);
       const u32 coff = val | ((type == 1 ? c >> 5 : 0u) << 8);
       const u32 avail = n_in - ip - 1;
       // literal bytes present (:761) / copy offset in range (:1200,1410,1466),
@@ -282,13 +299,14 @@ __global__ __launch_bounds__(64) void index_kernel(
       const u32 b_cp = (coff - 1u >= op) ? 1u : 0u;
       const bool bad = (avail < nb) | (expected - op < len) |  // writer overrun
                        (((b_lit & litm) | (b_cp & ~litm)) != 0);
-      const bool look = ip < lim;
       status = (look && bad) ? kCorrupt : status;
-      lim = (look && bad) ? 0u : lim;
       const bool take = look && !bad;
-      if (bm) atomicOr(&bmr[((ip >> 5) & 15) * kWave + lane], take ? 1u << (ip & 31) : 0u);
-      ip += take ? 1 + nb + (len & litm) : 0u;
-      op += take ? len : 0u;
+      // unconditional (bits land in the LDS ring even without a bitmap): a
+      // per-tag branch here would split the unrolled walk into one basic
+      // block per tag
+      atomicOr(&bmr[((ip >> 5) & 15) * kWave + lane], take ? 1u << (ip & 31) : 0u);
+      op += look ? len : 0u;
+      ip = ip_next;
     }
     // end of input between tags (RefillTag eof): the result, snappy.cc:858-868
     if (status < 0 && ip == n_in) status = op == expected ? kOk : kCorrupt;
