@@ -265,6 +265,7 @@ __global__ __launch_bounds__(64) void index_kernel(
     };
     u32 lo, hi;
     ring_read(ip, lo, hi);
+    const u32 op_it = op;
 #pragma unroll
     for (int j = 0; j < kIdxTags; ++j) {
       const u32 bsh = (ip + ibal) & 3;
@@ -289,16 +290,15 @@ __global__ __launch_bounds__(64) void index_kernel(
       // walk reads from there on only sets bits in the LDS ring, which are
       // never stored for a corrupt message, and ring indices are masked.
       const bool look = ip < lim;
-      const u32 ip_next = ip + (look ? 1 + nb + (len & litm) : 0u);
+      const u32 nx = ip + 1 + nb + (len & litm);
+      const u32 ip_next = look ? nx : ip;
       if (j + 1 < kIdxTags) ring_read(ip_next, lo, hi);
       const u32 coff = val | ((type == 1 ? c >> 5 : 0u) << 8);
-      const u32 avail = n_in - ip - 1;
-      // literal bytes present (:761) / copy offset in range (:1200,1410,1466),
-      // merged by mask rather than by a branch
-      const u32 b_lit = (avail - nb < len) ? 1u : 0u;
-      const u32 b_cp = (coff - 1u >= op) ? 1u : 0u;
-      const bool bad = (avail < nb) | (expected - op < len) |  // writer overrun
-                       (((b_lit & litm) | (b_cp & ~litm)) != 0);
+      // tag bytes and literal bytes present (:744-761): the next tag position
+      // is inside the input (nx < ip only when a 4-byte literal length wrapped
+      // it); copy offset in range (:1200, 1410, 1466).  The writer's space
+      // check (:1166, :1400) is per iteration, below: op only grows.
+      const bool bad = (nx > n_in) | (nx < ip) | ((coff - 1u >= op) & (type != 0));
       status = (look && bad) ? kCorrupt : status;
       const bool take = look && !bad;
       // unconditional (bits land in the LDS ring even without a bitmap): a
@@ -308,6 +308,9 @@ __global__ __launch_bounds__(64) void index_kernel(
       op += look ? len : 0u;
       ip = ip_next;
     }
+    // writer space (:1166, :1400), checked once per iteration: op only grows,
+    // and one iteration cannot wrap it (accepted literals fit the input)
+    if (status < 0 && (op > expected || op < op_it)) status = kCorrupt;
     // end of input between tags (RefillTag eof): the result, snappy.cc:858-868
     if (status < 0 && ip == n_in) status = op == expected ? kOk : kCorrupt;
 
