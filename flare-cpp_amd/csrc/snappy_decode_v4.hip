@@ -46,7 +46,7 @@ constexpr u32 kRingChunks = 16;              // 16-byte chunks per lane (256 B)
 constexpr u32 kRingDwords = kRingChunks * 4;
 constexpr u32 kAhead = 7;                    // chunks prefetched per iteration
 
-// ---- pass 1b (index_big_kernel) geometry
+// ---- pass 1b (index_big_message, run by exec_kernel's large-message waves) geometry
 constexpr u32 kBigIndexMin = 8 * 1024;       // large: compressed size above
 constexpr u32 kBigIndexMax = 48 * 1024;      // clamp(4 x the batch mean, min, max)
 constexpr u32 kHugeIndexBytes = 256 * 1024;  // large ones handed out first
@@ -58,6 +58,9 @@ constexpr u32 kWavesPerBlock = 4;
 constexpr u32 kTagRing = 512;                // tag positions per wave (LDS)
 constexpr u32 kFillWords = 16;               // bitmap words per fill (512 input bytes)
 constexpr u32 kMaxPieces = 64;
+// bm_base[m] with this bit set: the message is one literal starting at the
+// low bits (set by pass 1; bitmap bases stay below 2^31 words)
+constexpr u32 kSingleLiteral = 0x80000000u;
 
 __device__ u32x4 g_dummy_chunk[1];
 
@@ -179,7 +182,7 @@ __global__ __launch_bounds__(64) void index_kernel(
     if (valid_msg) bm_base_out[m] = bm_base;
   }
 
-  // ---- large messages go to index_big_kernel (a whole wave per message);
+  // ---- large messages go to index_big_message (a whole wave per message);
   // one lane would walk them serially for tens of milliseconds
   if (big_list) {
     // the largest ones (> kHugeIndexBytes) are listed from the end of the
@@ -215,6 +218,11 @@ __global__ __launch_bounds__(64) void index_kernel(
     for (int i = 0; i < 4; ++i) ring[(d + i) * kWave + lane] = v[i];
     ring[(d == 0 ? kRingDwords : kRingDwords + 1) * kWave + lane] = v[0];
   };
+  // Single-literal message (random bodies: the encoder emits one literal when
+  // it finds no match): its first tag is a literal whose bytes end the input.
+  // Decided here from the first chunks, once per message; pass 2 copies such
+  // a message without walking the bitmap (bm_base = kSingleLiteral | source).
+  u32 single_src = 0;
   if (status < 0) {
     u32x4 c0[4];
 #pragma unroll
@@ -225,6 +233,21 @@ __global__ __launch_bounds__(64) void index_kernel(
 #pragma unroll
     for (u32 c = 0; c < 4; ++c) ring_write(c, c0[c], c <= last_chunk);
     wend = iend = (last_chunk + 1 < 4) ? last_chunk + 1 : 4;
+    // tag byte at ip (header <= 5 bytes) and its <= 4 length bytes lie in the
+    // first 32 bytes of the aligned chunks (ibal + 9 < 32)
+    const u32 P = ip + ibal;
+    const u32 w[8] = {c0[0][0], c0[0][1], c0[0][2], c0[0][3], c0[1][0], c0[1][1], c0[1][2], c0[1][3]};
+    const u32 d = P >> 2;
+    const u32 w0 = mux8(w, d), w1 = mux8(w, d + 1), w2 = d + 2 < 8 ? mux8(w, d + 2) : 0u;
+    const u32 t0 = alignbyte(w1, w0, P & 3);
+    const u32 ext = alignbyte(alignbyte(w2, w1, P & 3), t0, 1);
+    const u32 c = t0 & 0xffu;
+    const u32 l0 = (c >> 2) + 1;
+    const u32 nbl = l0 > 60 ? l0 - 60 : 0u;
+    const u32 val = ext & (0xffffffffu >> ((32 - 8 * nbl) & 31));
+    const u32 len = nbl ? val + 1u : l0;
+    const u64 end = (u64)ip + 1 + nbl + len;
+    if ((c & 3) == 0 && end == n_in && ip < n_in && len == expected) single_src = ip + 1 + nbl;
   }
 
   u32 op = 0;
@@ -362,6 +385,7 @@ __global__ __launch_bounds__(64) void index_kernel(
     more = __any(status < 0);
   }
   if (valid_msg) status_out[m] = status;
+  if (valid_msg && bitmap && status == kOk && single_src) bm_base_out[m] = kSingleLiteral | single_src;
 }
 
 // ===========================================================================
@@ -376,133 +400,112 @@ __global__ __launch_bounds__(64) void index_kernel(
 // prefix sum, and the position-dependent checks run on all of them at once.
 // Input is staged into LDS 5 KiB at a time.
 // ===========================================================================
-__global__ __launch_bounds__(4 * 64) void index_big_kernel(
-    const u8* __restrict__ in, const u64* __restrict__ in_off,
-    const u32* __restrict__ in_len, const u32* __restrict__ out_len, u32 flags,
-    i32* __restrict__ status_out, const u32* __restrict__ bm_base,
-    u32* __restrict__ bitmap, const u32* __restrict__ big_count,
-    const u32* __restrict__ big_list, u32* __restrict__ big_next, u32 n_msgs) {
-  __shared__ u32 stage_s[4][kBigStageBytes / 4 + 4];
-  // wave index made visibly uniform, so the per-message walk state (ip, op,
-  // status, sizes) lives in SGPRs and the walk is scalar code
-  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const u32 lane = threadIdx.x & 63;
-  u32* st = stage_s[wv];
-  const bool strict = flags & 2u;
-  const u32 n_huge = big_count[8];
-  const u32 count = big_count[0] + n_huge;
+// Indexes message m (listed by pass 1) with the calling wave: writes its
+// bitmap bits and returns its final status.  `st` is the wave's LDS stage
+// (kBigStageBytes + 16 bytes).
+__device__ __forceinline__ i32 index_big_message(
+    u32 m, const u8* __restrict__ in, const u64* __restrict__ in_off,
+    const u32* __restrict__ in_len, const u32* __restrict__ out_len, bool strict,
+    const u32* __restrict__ bm_base, u32* __restrict__ bitmap, u32* st, u32 lane) {
+  const u8* ib = in + in_off[m];
+  const u32 n_in = in_len[m];
+  const u32 expected = out_len[m];
+  u32 ulen = 0;
+  u32 ip = (u32)parse_varint_header(ib, n_in, strict, &ulen);  // pass 1 accepted it
+  u32 op = 0;
+  i32 status = -1;
+  u32* bm = bitmap + bm_base[m];
+  const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
+  const u8* abase = ib - ibal;
+  const u32 last_chunk = (ibal + n_in - 1) >> 4;
+  int spos = -1;  // message position of stage byte 0 (-1: nothing staged)
+  u32 send = 0;   // positions [spos, send) are valid in the stage
 
-  // messages are handed out one at a time from a counter: sizes are
-  // power-law distributed, a static stride leaves a few waves with most of
-  // the bytes
-  // (every lane takes part in the atomic, adding 1 for lane 0 and 0 for the
-  // rest, so no lane-0-only branch exists for the compiler to fold the
-  // broadcast into; lane 0's result is the wave's index)
-  for (;;) {
-    const u32 got = atomicAdd(big_next, lane == 0 ? 1u : 0u);
-    const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
-    if (idx >= count) break;
-    const u32 m = idx < n_huge ? big_list[n_msgs - 1 - idx] : big_list[idx - n_huge];
-    const u8* ib = in + in_off[m];
-    const u32 n_in = in_len[m];
-    const u32 expected = out_len[m];
-    u32 ulen = 0;
-    u32 ip = (u32)parse_varint_header(ib, n_in, strict, &ulen);  // pass 1 accepted it
-    u32 op = 0;
-    i32 status = -1;
-    u32* bm = bitmap + bm_base[m];
-    const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
-    const u8* abase = ib - ibal;
-    const u32 last_chunk = (ibal + n_in - 1) >> 4;
-    int spos = -1;  // message position of stage byte 0 (-1: nothing staged)
-    u32 send = 0;   // positions [spos, send) are valid in the stage
-
-    while (status < 0) {
-      if (ip >= n_in) {  // end of input between tags (snappy.cc:858-868)
-        status = (ip == n_in && op == expected) ? kOk : kCorrupt;
-        break;
-      }
-      const u32 wb = ip & ~31u;
-      // ---------- stage input covering [wb, wb + 64 + 4)
-      if (spos < 0 || wb < (u32)spos || wb + 72 > send) {
-        const u32 c0 = (wb + ibal) >> 4;
-        u32x4 x[kBigStageChunks / 64];
-#pragma unroll
-        for (u32 r = 0; r < kBigStageChunks / 64; ++r) {
-          u32 k = c0 + r * 64 + lane;
-          k = k <= last_chunk ? k : last_chunk;
-          x[r] = *reinterpret_cast<const u32x4*>(abase + 16 * k);
-        }
-        wave_lds_fence();  // previous window's stage reads are done
-#pragma unroll
-        for (u32 r = 0; r < kBigStageChunks / 64; ++r)
-          *reinterpret_cast<u32x4*>(st + 4 * (r * 64 + lane)) = x[r];
-        wave_lds_fence();
-        spos = (int)(16 * c0) - (int)ibal;
-        send = (u32)spos + kBigStageBytes - 8;
-      }
-      // ---------- every lane decodes the tag that would start at wb + lane
-      const u32 p = wb + lane;
-      const u32 s = p - (u32)spos;
-      const u32 dw = s >> 2, bsh = s & 3;
-      const u32 lo = st[dw], hi = st[dw + 1];
-      const u32 t0 = alignbyte(hi, lo, bsh);
-      const u32 b4 = (hi >> (8 * bsh)) & 0xffu;
-      const u32 c = t0 & 0xffu;
-      const u32 type = c & 3;
-      const bool is_lit = type == 0;
-      const u32 l0 = (c >> 2) + 1;
-      const bool longlit = is_lit & (l0 >= 61);
-      const u32 nb = is_lit ? (longlit ? l0 - 60 : 0u) : (1u << (type - 1));
-      const u32 ext = (b4 << 24) | (t0 >> 8);
-      const u32 val = nb >= 4 ? ext : ext & ((1u << (8 * nb)) - 1u);
-      const u32 len = is_lit ? (longlit ? val + 1u : l0) : (type == 1 ? 4 + ((c >> 2) & 7) : l0);
-      const u32 coff = type == 1 ? (((c >> 5) << 8) | val) : val;
-      const u32 avail = n_in - p - 1;
-      // the checks that need no walk state: tag bytes and literal bytes present
-      const bool bad_local = (p >= n_in) | (avail < nb) | (is_lit & (avail - nb < len));
-      const u32 adv = 1 + nb + (is_lit ? len : 0u);
-      const u32 nxt = p + adv;  // next tag position (meaningful when !bad_local)
-
-      // ---------- which lanes are real tag starts: the chain from ip, by
-      // pointer doubling.  J = successor lane (64 = left the window, or reached
-      // the end of input); after round k, M = the lanes visited within 2^k
-      // steps from this lane.  A 64-byte window holds <= 32 tags (>= 2 bytes
-      // each), so 5 rounds cover any chain.
-      u32 J = (bad_local || adv >= 64 - lane || nxt >= n_in) ? 64u : lane + adv;
-      u64 M = 1ull << lane;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const u32 src = J < 64 ? J : lane;
-        const u64 Mj = ((u64)(u32)__shfl((int)(u32)(M >> 32), (int)src, 64) << 32) |
-                       (u32)__shfl((int)(u32)M, (int)src, 64);
-        const u32 Jj = (u32)__shfl((int)J, (int)src, 64);
-        if (J < 64) {
-          M |= Mj;
-          J = Jj;
-        }
-      }
-      const u32 first = ip - wb;
-      const u64 S = ((u64)readlane((u32)(M >> 32), first) << 32) | readlane((u32)M, first);
-      const bool in_s = (S >> lane) & 1ull;
-      // output position of each chain tag: op + exclusive prefix sum of lengths
-      const u32 lv = in_s ? len : 0u;
-      const u32 t_op = op + dpp_incl_scan(lv) - lv;
-      // writer space and copy offset checks (:761, :1166, :1200, :1410, :1466);
-      // the first failing tag has an exact t_op (every earlier one passed)
-      const bool bad = in_s && (bad_local || expected - t_op < len || (!is_lit && coff - 1u >= t_op));
-      if (__any(bad)) {
-        status = kCorrupt;
-        break;
-      }
-      const u32 last = 63u - (u32)__builtin_clzll(S);
-      ip = readlane(nxt, last);
-      op = readlane(t_op + len, last);
-      const u32 wbits = lane == 0 ? (u32)S : (u32)(S >> 32);
-      if (lane < 2 && wbits) bm[(wb >> 5) + lane] = wbits;
+  while (status < 0) {
+    if (ip >= n_in) {  // end of input between tags (snappy.cc:858-868)
+      status = (ip == n_in && op == expected) ? kOk : kCorrupt;
+      break;
     }
-    if (lane == 0) status_out[m] = status;
+    const u32 wb = ip & ~31u;
+    // ---------- stage input covering [wb, wb + 64 + 4)
+    if (spos < 0 || wb < (u32)spos || wb + 72 > send) {
+      const u32 c0 = (wb + ibal) >> 4;
+      u32x4 x[kBigStageChunks / 64];
+#pragma unroll
+      for (u32 r = 0; r < kBigStageChunks / 64; ++r) {
+        u32 k = c0 + r * 64 + lane;
+        k = k <= last_chunk ? k : last_chunk;
+        x[r] = *reinterpret_cast<const u32x4*>(abase + 16 * k);
+      }
+      wave_lds_fence();  // previous window's stage reads are done
+#pragma unroll
+      for (u32 r = 0; r < kBigStageChunks / 64; ++r)
+        *reinterpret_cast<u32x4*>(st + 4 * (r * 64 + lane)) = x[r];
+      wave_lds_fence();
+      spos = (int)(16 * c0) - (int)ibal;
+      send = (u32)spos + kBigStageBytes - 8;
+    }
+    // ---------- every lane decodes the tag that would start at wb + lane
+    const u32 p = wb + lane;
+    const u32 s = p - (u32)spos;
+    const u32 dw = s >> 2, bsh = s & 3;
+    const u32 lo = st[dw], hi = st[dw + 1];
+    const u32 t0 = alignbyte(hi, lo, bsh);
+    const u32 b4 = (hi >> (8 * bsh)) & 0xffu;
+    const u32 c = t0 & 0xffu;
+    const u32 type = c & 3;
+    const bool is_lit = type == 0;
+    const u32 l0 = (c >> 2) + 1;
+    const bool longlit = is_lit & (l0 >= 61);
+    const u32 nb = is_lit ? (longlit ? l0 - 60 : 0u) : (1u << (type - 1));
+    const u32 ext = (b4 << 24) | (t0 >> 8);
+    const u32 val = nb >= 4 ? ext : ext & ((1u << (8 * nb)) - 1u);
+    const u32 len = is_lit ? (longlit ? val + 1u : l0) : (type == 1 ? 4 + ((c >> 2) & 7) : l0);
+    const u32 coff = type == 1 ? (((c >> 5) << 8) | val) : val;
+    const u32 avail = n_in - p - 1;
+    // the checks that need no walk state: tag bytes and literal bytes present
+    const bool bad_local = (p >= n_in) | (avail < nb) | (is_lit & (avail - nb < len));
+    const u32 adv = 1 + nb + (is_lit ? len : 0u);
+    const u32 nxt = p + adv;  // next tag position (meaningful when !bad_local)
+
+    // ---------- which lanes are real tag starts: the chain from ip, by
+    // pointer doubling.  J = successor lane (64 = left the window, or reached
+    // the end of input); after round k, M = the lanes visited within 2^k
+    // steps from this lane.  A 64-byte window holds <= 32 tags (>= 2 bytes
+    // each), so 5 rounds cover any chain.
+    u32 J = (bad_local || adv >= 64 - lane || nxt >= n_in) ? 64u : lane + adv;
+    u64 M = 1ull << lane;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const u32 src = J < 64 ? J : lane;
+      const u64 Mj = ((u64)(u32)__shfl((int)(u32)(M >> 32), (int)src, 64) << 32) |
+                     (u32)__shfl((int)(u32)M, (int)src, 64);
+      const u32 Jj = (u32)__shfl((int)J, (int)src, 64);
+      if (J < 64) {
+        M |= Mj;
+        J = Jj;
+      }
+    }
+    const u32 first = ip - wb;
+    const u64 S = ((u64)readlane((u32)(M >> 32), first) << 32) | readlane((u32)M, first);
+    const bool in_s = (S >> lane) & 1ull;
+    // output position of each chain tag: op + exclusive prefix sum of lengths
+    const u32 lv = in_s ? len : 0u;
+    const u32 t_op = op + dpp_incl_scan(lv) - lv;
+    // writer space and copy offset checks (:761, :1166, :1200, :1410, :1466);
+    // the first failing tag has an exact t_op (every earlier one passed)
+    const bool bad = in_s && (bad_local || expected - t_op < len || (!is_lit && coff - 1u >= t_op));
+    if (__any(bad)) {
+      status = kCorrupt;
+      break;
+    }
+    const u32 last = 63u - (u32)__builtin_clzll(S);
+    ip = readlane(nxt, last);
+    op = readlane(t_op + len, last);
+    const u32 wbits = lane == 0 ? (u32)S : (u32)(S >> 32);
+    if (lane < 2 && wbits) bm[(wb >> 5) + lane] = wbits;
   }
+  return status;
 }
 
 // ===========================================================================
@@ -540,16 +543,38 @@ __device__ __forceinline__ void exec_message(
     u32 m, const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u8* out, const u64* __restrict__ out_off,
     const u32* __restrict__ out_len, i32* __restrict__ status, const u32* __restrict__ bm_base,
-    const u32* __restrict__ bitmap, u32* ring, u8* pmap, u8* sb, const u32x4* sel_tab, u32 lane) {
-  if (status[m] != kOk) return;
-
+    const u32* __restrict__ bitmap, u32* ring, u8* pmap, u8* sb, const u32x4* sel_tab, u32 lane,
+    i32 st) {
+  // every per-message scalar is loaded up front (one round trip, not a chain)
+  const u32 bmb = bm_base[m];
   const u32 n_in = in_len[m];
   const u32 expected = out_len[m];
   const u8* ib = in + in_off[m];
   u8* ob = out + out_off[m];
+  if (st != kOk) return;
   const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
   const u32 obal = (u32)(reinterpret_cast<uintptr_t>(ob) & 15);
-  const u32* bm = bitmap + bm_base[m];
+
+  if (bmb & kSingleLiteral) {
+    // one literal (checked by pass 1): a straight copy, 4 KiB per step with
+    // all loads first
+    const u32 S = bmb & ~kSingleLiteral;
+    for (u32 k0 = 0; k0 < expected; k0 += 4096) {
+      u32x4 x[4];
+#pragma unroll
+      for (u32 r = 0; r < 4; ++r) {
+        const u32 k = k0 + 1024 * r + lane * 16;
+        x[r] = k < expected ? load16_clamped(ib, S + k, n_in, ibal) : u32x4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (u32 r = 0; r < 4; ++r) {
+        const u32 k = k0 + 1024 * r + lane * 16;
+        if (k < expected) store_exact(ob + k, x[r], expected - k < 16 ? expected - k : 16u);
+      }
+    }
+    return;
+  }
+  const u32* bm = bitmap + bmb;
   const u32 nwords = (n_in + 31) >> 5;
 
 #ifdef FSG_STAMPS
@@ -817,13 +842,16 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     const u32* __restrict__ in_len, u32 n_msgs, u8* out,
     const u64* __restrict__ out_off, const u32* __restrict__ out_len,
     i32* __restrict__ status, const u32* __restrict__ bm_base,
-    const u32* __restrict__ bitmap, const u32* __restrict__ big_count,
+    u32* __restrict__ bitmap, const u32* __restrict__ big_count,
     const u32* __restrict__ big_list, u32* __restrict__ exec_next, u32 big_blocks,
-    u32 big_threshold) {
-  __shared__ u32 ring_s[kWavesPerBlock][kTagRing];
+    u32 big_threshold, u32 flags) {
+  const bool strict = flags & 2u;
+  // per wave: the tag ring, then the output window; a large message's index
+  // walk stages its input over both (kBigStageBytes + 16 <= their size)
+  __shared__ __attribute__((aligned(16))) u8 wl_s[kWavesPerBlock][4 * kTagRing + kWindow + 32];
   __shared__ u8 pmap_s[kWavesPerBlock][kMaxPieces];
-  __shared__ __attribute__((aligned(16))) u8 sb_s[kWavesPerBlock][kWindow + 32];
   __shared__ u32x4 sel_tab[16];
+  static_assert(kBigStageBytes + 16 <= 4 * kTagRing + kWindow + 32, "stage fits the wave's LDS");
 
   if (threadIdx.x < 64) init_pattern_table(sel_tab, threadIdx.x);
   __syncthreads();
@@ -833,15 +861,15 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
   // on them are scalar
   const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const u32 lane = threadIdx.x & 63;
-  u32* ring = ring_s[wv];
+  u32* ring = reinterpret_cast<u32*>(wl_s[wv]);
   u8* pmap = pmap_s[wv];
-  u8* sb = sb_s[wv];
+  u8* sb = wl_s[wv] + 4 * kTagRing;
 
   if (blockIdx.x >= big_blocks) {
     const u32 m = (blockIdx.x - big_blocks) * kWavesPerBlock + wv;
     if (m < n_msgs && in_len[m] <= big_threshold)
       exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring,
-                   pmap, sb, sel_tab, lane);
+                   pmap, sb, sel_tab, lane, status[m]);
     return;
   }
   const u32 n_huge = big_count[8];
@@ -852,8 +880,17 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
     if (idx >= nbig) break;
     const u32 m = idx < n_huge ? big_list[n_msgs - 1 - idx] : big_list[idx - n_huge];
+    // pass 1b for this message (the wave-parallel index walk), then its
+    // execution by the same wave.  The bitmap words just stored are read back
+    // by this wave: wait for the stores and drop this CU's L1 (another wave may
+    // have cached a neighbouring message's bitmap line); the status is passed
+    // on, not re-read through the scalar cache.
+    const i32 st = index_big_message(m, in, in_off, in_len, out_len, strict, bm_base, bitmap,
+                                     ring, lane);
+    if (lane == 0) status[m] = st;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, pmap,
-                 sb, sel_tab, lane);
+                 sb, sel_tab, lane, st);
   }
 }
 
@@ -889,7 +926,8 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   u32* bm_base = reinterpret_cast<u32*>(w + 256);
   u32* big_list = reinterpret_cast<u32*>(w + 256 + base_bytes);
   u32* bitmap = reinterpret_cast<u32*>(w + 256 + 2 * base_bytes);
-  const u64 cap_words = (ws_bytes - 256 - 2 * base_bytes) / 4;
+  u64 cap_words = (ws_bytes - 256 - 2 * base_bytes) / 4;
+  if (cap_words >= kSingleLiteral) cap_words = kSingleLiteral - 1;  // bases < 2^31 words
   // zero the counters and the bitmap (pass 1 writes only groups holding tags)
   hipError_t e = hipMemsetAsync(counter, 0, 256, stream);
   if (e == hipSuccess) e = hipMemsetAsync(bitmap, 0, cap_words * 4, stream);
@@ -906,16 +944,6 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
                                                       status, flags, counter, bm_base, bitmap,
                                                       cap_words, big_count, big_list, big_threshold);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  // large messages: one wave each, 4 per block; waves loop over the list
-  // (its length is only known on the device), so an empty list costs one
-  // short launch
-  {
-    const u32 blocks = n_msgs < 1024 ? (n_msgs + 3) / 4 : 256u;
-    index_big_kernel<<<blocks, 256, 0, stream>>>(in, in_off, in_len, out_len, flags, status,
-                                                 bm_base, bitmap, big_count, big_list,
-                                                 reinterpret_cast<u32*>(w + 128), n_msgs);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  }
   {
     // large-message blocks (empty when the batch has none: they exit after
     // one atomic), then one wave per message
@@ -923,7 +951,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     const u32 big_blocks = small_blocks < 256u ? small_blocks : 256u;
     exec_kernel<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap, big_count,
-        big_list, reinterpret_cast<u32*>(w + 192), big_blocks, big_threshold);
+        big_list, reinterpret_cast<u32*>(w + 192), big_blocks, big_threshold, flags);
   }
   return hipGetLastError();
 }

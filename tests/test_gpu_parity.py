@@ -345,3 +345,62 @@ def test_split_message_encode(gpu, oracle, cap):
         assert (st == 0).all() and all(o == x for o, x in zip(outs, items))
     finally:
         gpu.codec.set_split_region_cap(0)
+
+
+def _varint(n: int) -> bytes:
+    out = bytearray()
+    while True:
+        b = n & 0x7F
+        n >>= 7
+        out.append(b | (0x80 if n else 0))
+        if not n:
+            return bytes(out)
+
+
+def _literal(data: bytes, nbytes: int | None = None) -> bytes:
+    """A LITERAL tag (snappy.cc:156-196 form) with `nbytes` length bytes (0 =
+    length in the tag byte); non-minimal encodings are legal for the decoder."""
+    n = len(data) - 1
+    if nbytes is None:
+        nbytes = 0 if n < 60 else (n.bit_length() + 7) // 8
+    tag = (n << 2) if nbytes == 0 else ((59 + nbytes) << 2)
+    return bytes([tag]) + (n.to_bytes(nbytes, "little") if nbytes else b"") + data
+
+
+@pytest.mark.parametrize("variant", [0, 3, 4])
+def test_single_literal_streams(gpu, oracle, variant):
+    """Messages that are one literal take pass 2's straight-copy path (pass 1
+    marks them); near misses (truncated, trailing bytes, a second tag, header
+    disagreeing with the literal, non-minimal length bytes) must keep the
+    reference's verdict and bytes."""
+    import fsg as _f
+    rng = np.random.default_rng(11)
+    comps = []
+    for n in [1, 2, 15, 16, 17, 59, 60, 61, 64, 65, 255, 256, 257, 1000, 4096, 4097, 8191, 40000]:
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for nb in sorted({None, 1, 2, 3, 4} if n <= 256 else {None, 3, 4}, key=lambda x: -1 if x is None else x):
+            if nb is not None and n - 1 >= 1 << (8 * nb):
+                continue
+            s = _varint(n) + _literal(d, nb)
+            comps += [s, s[:-1], s + b"\x00", _varint(n + 1) + s[len(_varint(n)):],
+                      _varint(max(n - 1, 0)) + s[len(_varint(n)):]]
+        comps.append(_varint(n + 4) + _literal(d) + bytes([0x01 | (0 << 2), 1]))  # + COPY_1 len 4 off 1
+    # 4-byte length 0xffffffff wraps to a zero-length literal (uint32 arithmetic)
+    comps.append(b"\x00" + bytes([63 << 2]) + b"\xff\xff\xff\xff")
+    comps.append(b"\x05" + bytes([63 << 2]) + b"\xff\xff\xff\xff")
+    # 5-byte lenient header in front of a literal
+    comps.append(b"\x84\x80\x80\x80\x00" + _literal(b"abcd"))
+    gpu.codec.select_kernels(variant, 0)
+    try:
+        outs, ol, st = gpu.decompress(comps, [1 << 17] * len(comps))
+    finally:
+        gpu.codec.select_kernels(0, 0)
+    n_ok = 0
+    for i, (c, o, s) in enumerate(zip(comps, outs, st)):
+        ok, ulen, ref = oracle.uncompress(c, cap=1 << 17)
+        if not ok:
+            assert s in (_f.FSG_CORRUPT, _f.FSG_BAD_HEADER), (i, c[:8].hex(), s)
+        else:
+            n_ok += 1
+            assert s == _f.FSG_OK and o[:ulen] == ref, (i, c[:8].hex(), s)
+    assert n_ok > 40
