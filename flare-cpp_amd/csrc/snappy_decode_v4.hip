@@ -406,7 +406,8 @@ __global__ __launch_bounds__(64) void index_kernel(
 __device__ __forceinline__ i32 index_big_message(
     u32 m, const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, const u32* __restrict__ out_len, bool strict,
-    const u32* __restrict__ bm_base, u32* __restrict__ bitmap, u32* st, u32 lane) {
+    const u32* __restrict__ bm_base, u32* __restrict__ bitmap, u32* st, u32 lane, u8* ob,
+    bool& seg) {
   const u8* ib = in + in_off[m];
   const u32 n_in = in_len[m];
   const u32 expected = out_len[m];
@@ -499,6 +500,18 @@ __device__ __forceinline__ i32 index_big_message(
       status = kCorrupt;
       break;
     }
+    // 64 KiB output segments for pass 2 (what the reference's encoder emits:
+    // fragments compressed independently, snappy.cc:875-954): no tag may
+    // span a boundary and no copy may reach below its own segment.  A tag
+    // starting exactly at a boundary stores its input offset in the slot's
+    // 4 bytes there; that segment's own output overwrites them in pass 2.
+    if (seg) {
+      const bool span = in_s && len > 0 && ((t_op ^ (t_op + len - 1)) >> 16) != 0;
+      const bool xcopy = in_s && !is_lit && t_op - coff < (t_op & ~0xffffu);
+      if (__any(span || xcopy)) seg = false;
+      if (seg && in_s && t_op != 0 && (t_op & 0xffffu) == 0 && t_op + 4 <= expected)
+        __builtin_memcpy(ob + t_op, &p, 4);
+    }
     const u32 last = 63u - (u32)__builtin_clzll(S);
     ip = readlane(nxt, last);
     op = readlane(t_op + len, last);
@@ -506,6 +519,67 @@ __device__ __forceinline__ i32 index_big_message(
     if (lane < 2 && wbits) bm[(wb >> 5) + lane] = wbits;
   }
   return status;
+}
+
+// Pass 1b launch: one wave per listed large message (taken from a counter,
+// huge ones first).  Each finished message goes to pass 2's work lists: its
+// 64 KiB segments (seg_list: m | k << 32 | last << 63) when the stream
+// allows them, else the whole message (whole_list).
+__global__ __launch_bounds__(4 * 64) void index_big_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off,
+    const u32* __restrict__ in_len, const u32* __restrict__ out_len, u32 flags,
+    i32* __restrict__ status_out, const u32* __restrict__ bm_base,
+    u32* __restrict__ bitmap, const u32* __restrict__ big_count,
+    const u32* __restrict__ big_list, u32* __restrict__ big_next, u32 n_msgs, u8* out,
+    const u64* __restrict__ out_off, u64* __restrict__ seg_list, u32* __restrict__ seg_count,
+    u32* __restrict__ whole_list, u32* __restrict__ whole_count) {
+  __shared__ u32 stage_s[4][kBigStageBytes / 4 + 4];
+  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const u32 lane = threadIdx.x & 63;
+  const bool strict = flags & 2u;
+  const u32 n_huge = big_count[8];
+  const u32 count = big_count[0] + n_huge;
+  if (count == 0) return;  // uniform batches: no atomics on the shared counter
+  for (;;) {  // all-lane atomic: lane 0 adds 1, lane 0's result is the index
+    const u32 got = atomicAdd(big_next, lane == 0 ? 1u : 0u);
+    const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
+    if (idx >= count) break;
+    const u32 m = idx < n_huge ? big_list[n_msgs - 1 - idx] : big_list[idx - n_huge];
+    bool seg = true;
+    const i32 st = index_big_message(m, in, in_off, in_len, out_len, strict, bm_base, bitmap,
+                                     stage_s[wv], lane, out + out_off[m], seg);
+    if (lane == 0) status_out[m] = st;
+    if (st != kOk) continue;
+    const u32 expected = out_len[m];
+    u32 nseg = 0;  // > 1: run as segments
+    if (seg && expected > 65536u) {
+      nseg = (expected + 65535u) >> 16;
+      if (expected - ((nseg - 1) << 16) < 4) --nseg;  // the tail joins the previous segment
+    }
+    bool whole = nseg < 2;
+    if (!whole) {
+      u32 b = 0;
+      if (lane == 0) b = atomicAdd(seg_count, nseg);
+      b = readlane(b, 0);
+      for (u32 k = lane; k < nseg; k += 64) {
+        const u64 e = b + k < n_msgs
+            ? ((u64)m | ((u64)k << 32) | ((u64)(k == nseg - 1) << 63))
+            : 0xffffffffull;  // past the list: dropped, the message runs whole
+        if (b + k < n_msgs) seg_list[b + k] = e;
+      }
+      if (b + nseg > n_msgs) {
+        // partly listed: the listed entries become holes
+        for (u32 k = lane; b + k < n_msgs && k < nseg; k += 64) seg_list[b + k] = 0xffffffffull;
+        whole = true;
+      }
+    }
+    if (whole) {
+      u32 b = 0;
+      if (lane == 0) b = atomicAdd(whole_count, 1u);
+      b = readlane(b, 0);
+      if (lane == 0) whole_list[b] = m;
+    }
+  }
 }
 
 // ===========================================================================
@@ -544,7 +618,10 @@ __device__ __forceinline__ void exec_message(
     const u32* __restrict__ in_len, u8* out, const u64* __restrict__ out_off,
     const u32* __restrict__ out_len, i32* __restrict__ status, const u32* __restrict__ bm_base,
     const u32* __restrict__ bitmap, u32* ring, u8* pmap, u8* sb, const u32x4* sel_tab, u32 lane,
-    i32 st) {
+    i32 st, u32 ip0, u32 op0, u32 op1) {
+  // One message (ip0 = op0 = 0, op1 = its length), or one segment of a large
+  // one: output [op0, op1) from the tags starting at input offset ip0, whose
+  // copies stay inside the segment (checked by the index walk).
   // every per-message scalar is loaded up front (one round trip, not a chain)
   const u32 bmb = bm_base[m];
   const u32 n_in = in_len[m];
@@ -555,7 +632,7 @@ __device__ __forceinline__ void exec_message(
   const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
   const u32 obal = (u32)(reinterpret_cast<uintptr_t>(ob) & 15);
 
-  if (bmb & kSingleLiteral) {
+  if ((bmb & kSingleLiteral) && op1 == expected && op0 == 0) {
     // one literal (checked by pass 1): a straight copy, 4 KiB per step with
     // all loads first
     const u32 S = bmb & ~kSingleLiteral;
@@ -581,15 +658,15 @@ __device__ __forceinline__ void exec_message(
   u64 st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u64 t_last_ = __builtin_amdgcn_s_memtime();
 #endif
-  u32 head = 0, tail = 0, scan = 0, op = 0;
-  int sbase = -(int)obal;  // output position of sb[0]
-  u32 flushed = 0;         // output [0, flushed) is in global memory
+  u32 head = 0, tail = 0, scan = ip0 >> 5, op = op0;
+  int sbase = (int)((op0 + obal) & ~15u) - (int)obal;  // output position of sb[0]
+  u32 flushed = op0;  // output [op0, flushed) is in global memory
   // next fill, prefetched: lane l holds word scan + l / 4 and takes its byte l % 4
   auto fill_word = [&](u32 sc) -> u32 {
     const u32 wi = sc + (lane >> 2);
     return (lane < 4 * kFillWords && wi < nwords) ? bm[wi] : 0u;
   };
-  u32 bmw = fill_word(0);
+  u32 bmw = fill_word(scan);
   u32 pf_head = 0xffffffffu, pf_cnt = 0;  // tag bytes prefetched for ring [pf_head, +pf_cnt)
   u32x4 tv = u32x4{0, 0, 0, 0};
 
@@ -615,10 +692,12 @@ __device__ __forceinline__ void exec_message(
     // ---------- refill the tag ring from the bitmap (keeps >= 64 tags ahead)
     if (tail - head < 2 * kMaxPieces && scan < nwords) {
       u32 bits = (bmw >> (8 * (lane & 3))) & 0xffu;  // 8 bits per lane
+      const u32 bitbase = (scan + (lane >> 2)) * 32 + 8 * (lane & 3);
+      // a segment's walk starts at ip0: earlier tag starts are not its own
+      if (bitbase < ip0) bits &= bitbase + 8 <= ip0 ? 0u : (0xffu << (ip0 - bitbase)) & 0xffu;
       const u32 cnt = __builtin_popcount(bits);
       const u32 incl = dpp_incl_scan(cnt);
       u32 slot = tail + incl - cnt;
-      const u32 bitbase = (scan + (lane >> 2)) * 32 + 8 * (lane & 3);
       while (bits) {
         ring[slot & (kTagRing - 1)] = bitbase + __builtin_ctz(bits);
         ++slot;
@@ -632,7 +711,7 @@ __device__ __forceinline__ void exec_message(
       continue;
     }
     const u32 avail = tail - head;
-    if (avail == 0) break;
+    if (avail == 0 || op >= op1) break;
     const u32 take0 = avail < 64 ? avail : 64u;
     const bool valid = lane < take0;
     const u32 pos = valid ? ring[(head + lane) & (kTagRing - 1)] : 0u;
@@ -663,7 +742,7 @@ __device__ __forceinline__ void exec_message(
       // ---------- long literal: written straight to the slot by the whole
       // wave; the window restarts behind it
       const u32 L = readlane(len, 0), S = readlane(lsrc, 0);
-      if ((u64)op + L > expected) {  // writer overrun
+      if ((u64)op + L > op1) {  // writer overrun
         if (lane == 0) status[m] = kCorrupt;
         return;
       }
@@ -720,15 +799,15 @@ __device__ __forceinline__ void exec_message(
     const u32 lv = v ? len : 0u;
     const u32 incl = dpp_incl_scan(pc | (lv << 16));
     const u32 incl_pc = incl & 0xffffu, excl_pc = incl_pc - pc;
-    const bool fits = v && incl_pc <= kMaxPieces;
-    const u32 k_tags = (u32)__builtin_popcountll(__ballot(fits));
     const u32 t_op = op + (incl >> 16) - lv;
+    const bool fits = v && incl_pc <= kMaxPieces && t_op < op1;
+    const u32 k_tags = (u32)__builtin_popcountll(__ballot(fits));
     const u32 tot_pc = readlane(incl_pc, k_tags - 1);
     const u32 tot_len = readlane(incl >> 16, k_tags - 1);
     // copy offset 0 or past the bytes produced so far: the reference's
     // writer check (snappy.cc:1200, :1410, :1466); the message is corrupt
     // and the writer's space check (:1166, :1400) against the header length
-    if (__any(v && ((u64)t_op + len > expected || (!is_lit && (coff == 0 || coff > t_op))))) {
+    if (__any(fits && ((u64)t_op + len > op1 || (!is_lit && (coff == 0 || coff > t_op - op0))))) {
       if (lane == 0) status[m] = kCorrupt;
       return;
     }
@@ -820,11 +899,11 @@ __device__ __forceinline__ void exec_message(
 
     STAMP(5);
   }
-  if (op != expected) {  // the stream ended early (snappy.cc:858-868)
+  if (op != op1) {  // the stream ended early (snappy.cc:858-868)
     if (lane == 0) status[m] = kCorrupt;
     return;
   }
-  flush_to(expected);
+  flush_to(op1);
 #ifdef FSG_STAMPS
   if (lane == 0)
     for (int k = 0; k < 8; ++k) atomicAdd(&g_stamps[k], (unsigned long long)st_[k]);
@@ -842,10 +921,10 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     const u32* __restrict__ in_len, u32 n_msgs, u8* out,
     const u64* __restrict__ out_off, const u32* __restrict__ out_len,
     i32* __restrict__ status, const u32* __restrict__ bm_base,
-    u32* __restrict__ bitmap, const u32* __restrict__ big_count,
-    const u32* __restrict__ big_list, u32* __restrict__ exec_next, u32 big_blocks,
-    u32 big_threshold, u32 flags) {
-  const bool strict = flags & 2u;
+    u32* __restrict__ bitmap, const u32* __restrict__ seg_list,
+    const u32* __restrict__ seg_count, const u32* __restrict__ whole_list,
+    const u32* __restrict__ whole_count, u32* __restrict__ exec_next, u32 big_blocks,
+    u32 big_threshold) {
   // per wave: the tag ring, then the output window; a large message's index
   // walk stages its input over both (kBigStageBytes + 16 <= their size)
   __shared__ __attribute__((aligned(16))) u8 wl_s[kWavesPerBlock][4 * kTagRing + kWindow + 32];
@@ -869,28 +948,38 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     const u32 m = (blockIdx.x - big_blocks) * kWavesPerBlock + wv;
     if (m < n_msgs && in_len[m] <= big_threshold)
       exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring,
-                   pmap, sb, sel_tab, lane, status[m]);
+                   pmap, sb, sel_tab, lane, status[m], 0u, 0u, out_len[m]);
     return;
   }
-  const u32 n_huge = big_count[8];
-  const u32 nbig = big_count[0] + n_huge;
-  if (nbig == 0) return;
+  // large messages, listed by pass 1b: whole ones first (the longest start
+  // first), then 64 KiB segments of the others
+  const u32 n_whole = *whole_count;
+  const u32 n_seg_raw = *seg_count;
+  const u32 n_seg = n_seg_raw < n_msgs ? n_seg_raw : n_msgs;
+  const u32 total = n_whole + n_seg;
+  if (total == 0) return;
+  const u64* segs = reinterpret_cast<const u64*>(seg_list);
   for (;;) {  // all-lane atomic: lane 0 adds 1, lane 0's result is the index
     const u32 got = atomicAdd(exec_next, lane == 0 ? 1u : 0u);
     const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
-    if (idx >= nbig) break;
-    const u32 m = idx < n_huge ? big_list[n_msgs - 1 - idx] : big_list[idx - n_huge];
-    // pass 1b for this message (the wave-parallel index walk), then its
-    // execution by the same wave.  The bitmap words just stored are read back
-    // by this wave: wait for the stores and drop this CU's L1 (another wave may
-    // have cached a neighbouring message's bitmap line); the status is passed
-    // on, not re-read through the scalar cache.
-    const i32 st = index_big_message(m, in, in_off, in_len, out_len, strict, bm_base, bitmap,
-                                     ring, lane);
-    if (lane == 0) status[m] = st;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (idx >= total) break;
+    if (idx < n_whole) {
+      const u32 m = whole_list[idx];
+      exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring,
+                   pmap, sb, sel_tab, lane, status[m], 0u, 0u, out_len[m]);
+      continue;
+    }
+    const u64 e = segs[idx - n_whole];
+    const u32 m = (u32)e;
+    if (m == 0xffffffffu) continue;  // a hole (the message runs whole)
+    const u32 k = (u32)(e >> 32) & 0x7fffffffu;
+    const u32 expected = out_len[m];
+    const u32 op0 = k << 16;
+    const u32 op1 = (e >> 63) ? expected : op0 + 65536u;
+    u32 ip0 = 0;  // segment k > 0 starts at the input offset pass 1b left in its slot
+    if (k) __builtin_memcpy(&ip0, out + out_off[m] + op0, 4);
     exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, pmap,
-                 sb, sel_tab, lane, st);
+                 sb, sel_tab, lane, status[m], ip0, op0, op1);
   }
 }
 
@@ -906,11 +995,14 @@ extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
 #endif
 
 // Workspace: [0, 256) counters (bitmap bump allocator at 0, large-message
-// count at 64, huge-message count at 96, queue heads at 128 and 192) | bm_base[n] | big_list[n] | bitmap words.
+// count at 64, huge-message count at 96, queue heads at 128 and 192, segment
+// count at 160, whole-message count at 224) | bm_base[n] | big_list[n] |
+// seg_list[n] (u64) | whole_list[n] | bitmap words.
+constexpr u64 kListBases = 5;  // u32 arrays of n entries before the bitmap
 size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
   const u64 words = total_in_bytes / 32 + 4ull * n_msgs + 64;
-  return (size_t)(256 + 2 * base_bytes + 4 * words);
+  return (size_t)(256 + kListBases * base_bytes + 4 * words);
 }
 
 hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
@@ -920,13 +1012,15 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   if (n_msgs == 0) return hipSuccess;
   u8* w = static_cast<u8*>(ws);
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
-  if (ws_bytes < 256 + 2 * base_bytes + 4 * 64) return hipErrorInvalidValue;
+  if (ws_bytes < 256 + kListBases * base_bytes + 4 * 64) return hipErrorInvalidValue;
   u32* counter = reinterpret_cast<u32*>(w);
   u32* big_count = reinterpret_cast<u32*>(w + 64);
   u32* bm_base = reinterpret_cast<u32*>(w + 256);
   u32* big_list = reinterpret_cast<u32*>(w + 256 + base_bytes);
-  u32* bitmap = reinterpret_cast<u32*>(w + 256 + 2 * base_bytes);
-  u64 cap_words = (ws_bytes - 256 - 2 * base_bytes) / 4;
+  u64* seg_list = reinterpret_cast<u64*>(w + 256 + 2 * base_bytes);
+  u32* whole_list = reinterpret_cast<u32*>(w + 256 + 4 * base_bytes);
+  u32* bitmap = reinterpret_cast<u32*>(w + 256 + kListBases * base_bytes);
+  u64 cap_words = (ws_bytes - 256 - kListBases * base_bytes) / 4;
   if (cap_words >= kSingleLiteral) cap_words = kSingleLiteral - 1;  // bases < 2^31 words
   // zero the counters and the bitmap (pass 1 writes only groups holding tags)
   hipError_t e = hipMemsetAsync(counter, 0, 256, stream);
@@ -944,14 +1038,31 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
                                                       status, flags, counter, bm_base, bitmap,
                                                       cap_words, big_count, big_list, big_threshold);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  // pass 1b: large messages, one wave each (an empty list costs one short
+  // launch); they land in pass 2's work lists
   {
-    // large-message blocks (empty when the batch has none: they exit after
-    // one atomic), then one wave per message
+    const u32 q = (n_msgs + 3) / 4;
+    const u32 blocks = q < 1024u ? q : 1024u;
+    index_big_kernel<<<blocks, 256, 0, stream>>>(
+        in, in_off, in_len, out_len, flags, status, bm_base, bitmap, big_count, big_list,
+        reinterpret_cast<u32*>(w + 128), n_msgs, out, out_off, seg_list,
+        reinterpret_cast<u32*>(w + 160), whole_list, reinterpret_cast<u32*>(w + 224));
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  {
+    // large-message blocks (exit after one atomic when the lists are empty),
+    // then one wave per message
     const u32 small_blocks = (n_msgs + kWavesPerBlock - 1) / kWavesPerBlock;
-    const u32 big_blocks = small_blocks < 256u ? small_blocks : 256u;
+    static const u32 kBigBlocks = [] {  // A/B knob
+      const char* e = getenv("FSG_EXEC_BIG_BLOCKS");
+      return e ? (u32)atoi(e) : 512u;
+    }();
+    const u32 big_blocks = small_blocks < kBigBlocks ? small_blocks : kBigBlocks;
     exec_kernel<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(
-        in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap, big_count,
-        big_list, reinterpret_cast<u32*>(w + 192), big_blocks, big_threshold, flags);
+        in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
+        reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
+        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), big_blocks,
+        big_threshold);
   }
   return hipGetLastError();
 }

@@ -1,0 +1,17 @@
+#!/bin/bash
+# A/B of decode builds on one box plus an exec_kernel large-block-count sweep.
+mkdir -p gpurun_out/ab
+timeout -k 10 200 python -u -m pytest tests -m gpu -x -q --timeout 90 --timeout-method thread \
+  > gpurun_out/ab/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/ab/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/ab/pytest_gpu.log
+B="python bench.py --no-cpu-baseline --no-e2e --steps 10 --warmup 2 --verify-sample 16"
+run() {  # name lib workload [big_blocks]
+  FSG_EXEC_BIG_BLOCKS=${4:-256} FSG_LIB=$2 timeout -k 10 240 $B --workload $3 > gpurun_out/ab/$1_$3.json 2> gpurun_out/ab/$1_$3.err || return 1
+  echo "$1 $3 ${4:-256} $(python -c "import json,sys;d=json.load(open('gpurun_out/ab/$1_$3.json'));print(d['ms_per_step'], d['value'], d['correct']['oracle_sample_ok'], d['correct']['status_errors'])")"
+}
+L=flare-cpp_amd/lib/libflare_snappy_gpu.so
+P=build/ab/lib_prev.so
+run new $L cm-decompress 512 && run prev $P cm-decompress && run n768 $L cm-decompress 768 || exit 1
+for w in ${WLS:-c3-decompress c2-decompress}; do
+  run new $L $w && run prev $P $w && run new2 $L $w && run prev2 $P $w || exit 1
+done

@@ -404,3 +404,37 @@ def test_single_literal_streams(gpu, oracle, variant):
             n_ok += 1
             assert s == _f.FSG_OK and o[:ulen] == ref, (i, c[:8].hex(), s)
     assert n_ok > 40
+
+
+def _copy2(length: int, offset: int) -> bytes:
+    """COPY_2_BYTE_OFFSET tag (len 1..64, offset < 65536)."""
+    return bytes([((length - 1) << 2) | 2]) + offset.to_bytes(2, "little")
+
+
+def test_large_message_segments(gpu, oracle):
+    """Large bodies run in pass 2 as 64 KiB output segments when no tag spans
+    a segment boundary and no copy reaches below its segment (every stream the
+    reference encoder writes); otherwise whole.  Raw sizes around the
+    boundaries, a tail of < 4 bytes (joins the previous segment), and
+    hand-built streams that must run whole."""
+    rng = np.random.default_rng(5)
+    items = []
+    for n in (65537, 131072, 131073, 131074, 131075, 131076, 196609, 300000, 1 << 20):
+        items.append(fsg.make_batch(fsg.KIND_TEXT, [n], first_index=n).item(0))
+    comps = [oracle.compress(x) for x in items]
+    lit = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    # a copy at output 70000 reading 60000 (below its segment)
+    comps.append(_varint(len(lit) + 64) + _literal(lit) + _copy2(64, 10000))
+    # a copy spanning output 65536
+    lit2 = lit[:65500]
+    comps.append(_varint(65500 + 64 * 20) + _literal(lit2) + _copy2(64, 30000) * 20)
+    # segmentable hand-built stream: literal to the boundary, then copies inside segment 1
+    comps.append(_varint(65536 + 1000 + 640) + _literal(lit[:65536]) + _literal(lit[:1000])
+                 + _copy2(64, 1000) * 10)
+    comps += [oracle.compress(fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0))
+              for s in (100, 5000, 20000)]
+    outs, ol, st = gpu.decompress(comps, [1 << 21] * len(comps))
+    for i, (c, o, s) in enumerate(zip(comps, outs, st)):
+        ok, ulen, ref = oracle.uncompress(c, cap=1 << 21)
+        assert ok, i
+        assert s == fsg.FSG_OK and o[:ulen] == ref, (i, s)
