@@ -11,7 +11,7 @@ run() {  # name lib workload [big_blocks]
 }
 L=flare-cpp_amd/lib/libflare_snappy_gpu.so
 P=build/ab/lib_prev.so
-run new $L cm-decompress 512 && run prev $P cm-decompress 512 && run new2 $L cm-decompress 512 && run prev2 $P cm-decompress 512 || exit 1
+run new $L cm-decompress 512 && run prev $P cm-decompress 512 || exit 1
 for w in ${WLS:-c3-decompress c2-decompress}; do
   run new $L $w && run prev $P $w && run new2 $L $w && run prev2 $P $w || exit 1
 done
