@@ -208,15 +208,12 @@ int fsg_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
                   "fsg_decompress_batch");
   const bool v4_fits = d_workspace && workspace_bytes >= fsg::decode_v4_workspace_bytes(n_msgs, 0);
   if ((forced == 0 || forced == 4) && v4_fits) {
-    hipError_t e = fsg::launch_decode_v4(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
-                                         d_out_cap, d_out_len, d_status, flags, d_workspace,
-                                         workspace_bytes, (hipStream_t)stream);
-    // messages whose bitmap did not fit the workspace (status kNeedFallback)
-    if (e == hipSuccess)
-      e = fsg::launch_decode_v3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap,
-                                d_out_len, d_status, flags | fsg::kFlagFallbackOnly,
-                                (hipStream_t)stream);
-    return record(e, "fsg_decompress_batch");
+    // (messages whose bitmap does not fit the workspace are finished by the
+    // v4 launches' serial fallback pass)
+    return record(fsg::launch_decode_v4(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
+                                        d_out_cap, d_out_len, d_status, flags, d_workspace,
+                                        workspace_bytes, (hipStream_t)stream),
+                  "fsg_decompress_batch");
   }
   if (forced == 0 || forced == 3 || forced == 4)
     return record(fsg::launch_decode_v3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,

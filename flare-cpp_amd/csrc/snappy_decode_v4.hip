@@ -33,7 +33,8 @@
 // (same wave), so they observe them, exactly as v3's batches do.
 //
 // A message whose bitmap does not fit the workspace gets status kNeedFallback
-// in pass 1 and is decoded by the v3 kernel (kFlagFallbackOnly).
+// in pass 1 and is decoded serially by one lane in pass 3 (fallback_kernel).
+#include "snappy_lane_decode.h"
 #include "snappy_pieces.h"
 
 namespace fsg {
@@ -994,6 +995,25 @@ extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
+// Pass 3: the messages whose bitmap did not fit the workspace (status
+// kNeedFallback, header and slot already checked by pass 1), one lane each,
+// with the reference's serial tag loop.  A lean grid-sized launch: no LDS, a
+// status load per lane.  (Measured: a grid-sized launch here keeps the next
+// call's passes at full speed on C3, a one-block launch or none does not --
+// DESIGN.md section 5; the former v3 fallback launch cost 14 us more on C2.)
+__global__ __launch_bounds__(64) void fallback_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len,
+    u32 n_msgs, u8* out, const u64* __restrict__ out_off, const u32* __restrict__ out_len,
+    i32* __restrict__ status, u32 flags) {
+  const u32 m = blockIdx.x * 64 + threadIdx.x;
+  if (m >= n_msgs || status[m] != kNeedFallback) return;
+  const u8* ib = in + in_off[m];
+  const u32 n_in = in_len[m];
+  u32 ulen = 0;
+  const int h = parse_varint_header(ib, n_in, flags & 2u, &ulen);
+  status[m] = decode_one(ib + h, ib + n_in, out + out_off[m], out_len[m], true);
+}
+
 // Workspace: [0, 256) counters (bitmap bump allocator at 0, large-message
 // count at 64, huge-message count at 96, queue heads at 128 and 192, segment
 // count at 160, whole-message count at 224) | bm_base[n] | big_list[n] |
@@ -1063,7 +1083,10 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
         reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
         reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), big_blocks,
         big_threshold);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
   }
+  fallback_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off,
+                                                         out_len, status, flags);
   return hipGetLastError();
 }
 

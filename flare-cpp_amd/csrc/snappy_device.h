@@ -28,7 +28,8 @@ constexpr i32 kCorrupt = 1;
 constexpr i32 kBadHeader = 2;
 constexpr i32 kSlotTooSmall = 3;
 // Internal: message not indexed by the two-pass decoder (its bitmap did not
-// fit the workspace); finished by the v3 kernel under kFlagFallbackOnly.
+// fit the workspace); finished by v4's fallback_kernel (one lane, serial tag
+// loop), or by the v3 kernel under kFlagFallbackOnly.
 constexpr i32 kNeedFallback = 0x40000000;
 constexpr u32 kFlagFallbackOnly = 0x80000000u;
 // Internal: a large message left by the lane-per-message index pass for the
