@@ -5,12 +5,22 @@
 
 One "step" = one pass of the hot path over one batch resident in HBM.
 Default workload (the north-star target config): decompress
-65,536 x 64 KiB Zipf-text bodies.  Other workloads: c2-decompress (65,536 x
-4 KiB random), c3-compress, cm-decompress (power-law 256 B..1 MiB), c5-compress.
+65,536 x 64 KiB Zipf-text bodies; the same run also times C3 compress of the
+same bodies (the `encode` object).  Other workloads: c2-decompress (65,536 x
+4 KiB random), c3-compress, cm-decompress (power-law 256 B..1 MiB, strong
+scaling by default), c5-compress.
 
-For N > 1 launch with torch.distributed.run; each rank owns its own shard of
-messages (weak scaling, no data-path collective: messages are independent).
-Rank 0 prints ONE JSON line.
+Multi-GPU: one process per GPU.  `--gpus N` without a
+WORLD_SIZE in the environment makes this process a launcher: it spawns N
+ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1) before anything
+touches the GPU and exits with their status.  Under torch.distributed.run the
+environment is already set and the process is a rank.  Each rank owns a
+contiguous range of messages (weak: a full batch per rank; strong: one batch
+cut by cumulative bytes); there is no data-path collective.  RCCL carries the
+measurement collectives (MAX of times, SUM of counters), the all-gather of
+per-message (out_len, status), and the root-scatter variant (grouped
+send/recv of compressed shards from rank 0, reported beside the pre-placed
+rate).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -18,6 +28,9 @@ import argparse
 import hashlib
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -32,18 +45,19 @@ import shard  # noqa: E402
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+METRIC = "GiB/s device-resident Snappy decode+encode, batched RPC bodies, 1/2/4/8 GPU"
 
 WORKLOADS = {
-    # name: (op, kind, n_msgs, size spec, description)
-    "c3-decompress": ("decompress", fsg.KIND_TEXT, 65536, 65536,
+    # name: (op, kind, n_msgs, size spec, default scaling, description)
+    "c3-decompress": ("decompress", fsg.KIND_TEXT, 65536, 65536, "weak",
                       "C3 decompress: 65,536 x 64 KiB Zipf-text bodies (~2.0x), device-resident"),
-    "c2-decompress": ("decompress", fsg.KIND_RANDOM, 65536, 4096,
+    "c2-decompress": ("decompress", fsg.KIND_RANDOM, 65536, 4096, "weak",
                       "C2 decompress: 65,536 x 4 KiB random bodies, device-resident"),
-    "c3-compress": ("compress", fsg.KIND_TEXT, 65536, 65536,
+    "c3-compress": ("compress", fsg.KIND_TEXT, 65536, 65536, "weak",
                     "C3 compress: 65,536 x 64 KiB Zipf-text bodies, device-resident"),
-    "cm-decompress": ("decompress", fsg.KIND_MIXED, 1 << 20, "mixed",
+    "cm-decompress": ("decompress", fsg.KIND_MIXED, 1 << 20, "mixed", "strong",
                       "CM decompress: 1,048,576 power-law bodies 256 B..1 MiB, 1 in 4 random"),
-    "c5-compress": ("compress", fsg.KIND_PROTO, 262144, "mixed",
+    "c5-compress": ("compress", fsg.KIND_PROTO, 262144, "mixed", "strong",
                     "C5 compress: 262,144 synthetic SnappyMessageProto responses"),
 }
 
@@ -51,30 +65,113 @@ WORKLOADS = {
 def kernel_source_hash() -> str:
     h = hashlib.sha256()
     for p in sorted((REPO / "flare-cpp_amd" / "csrc").glob("*")):
-        h.update(p.read_bytes())
+        if p.is_file():
+            h.update(p.read_bytes())
     return h.hexdigest()[:16]
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c3-decompress", choices=sorted(WORKLOADS))
-    ap.add_argument("--n-msgs", type=int, default=0, help="override messages per GPU")
+    ap.add_argument("--n-msgs", type=int, default=0, help="override messages per GPU (weak) / total (strong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-encode", action="store_true", help="skip the encode leg of a decompress run")
+    ap.add_argument("--no-root-scatter", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--verify-sample", type=int, default=64)
-    ap.add_argument("--decode-lanes", type=int, default=-1,
-                    help="lanes in flight for the persistent decoder (-1 = library default)")
     ap.add_argument("--decode-kernel", type=int, default=0,
-                    help="decoder variant (0 = library default, 1-4 = force; A/B runs)")
+                    help="decoder variant (0 = library default, 1/3/4 = force; A/B runs)")
     ap.add_argument("--encode-kernel", type=int, default=0,
-                    help="encoder variant (0 = library default, 1-3 = force; A/B runs)")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="weak: every GPU owns a full batch; strong: one batch split by bytes")
-    return ap.parse_args()
+                    help="encoder variant (0 = library default, 1/3 = force; A/B runs)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
+                    help="weak: every GPU owns a full batch; strong: one batch split by bytes "
+                         "(default: per workload, strong for cm/c5)")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# Launcher: N ranks, spawned before any GPU call in this process.
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(nprocs: int, argv: list[str], entry: str | None = None, env_extra: dict | None = None,
+           timeout_s: float | None = None) -> int:
+    """Start `nprocs` ranks of `entry` (default: this file) with torchrun's
+    environment and wait for them.  A rank that fails ends the others (a
+    collective would otherwise wait for it forever).  Returns the worst exit
+    status."""
+    port = _free_port()
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_WORLD_SIZE=str(nprocs),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.update(env_extra or {})
+        procs.append(subprocess.Popen([sys.executable, entry or str(Path(__file__).resolve()), *argv], env=env))
+    t0 = time.time()
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0:
+                    rc = code if rc == 0 else rc
+                    for q in procs:
+                        q.terminate()
+            if timeout_s is not None and time.time() - t0 > timeout_s:
+                for q in procs:
+                    q.kill()
+                return 124
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
+# ---------------------------------------------------------------------------
+# Timing: HIP events on the codec's stream (GPU) or wall clock (the CPU test
+# ranks).
+
+class _Timer:
+    def __init__(self, torch, device, stream, n):
+        self.torch, self.gpu = torch, device.type == "cuda"
+        self.stream = stream
+        if self.gpu:
+            self.ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+        else:
+            self.t = [0.0] * (n + 1)
+
+    def mark(self, k):
+        if self.gpu:
+            self.ev[k].record(self.stream)
+        else:
+            self.t[k] = time.perf_counter()
+
+    def ms(self, k):
+        if self.gpu:
+            return self.ev[k].elapsed_time(self.ev[k + 1])
+        return (self.t[k + 1] - self.t[k]) * 1e3
+
+
+def _sync(torch, device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
 
 
 def batch_sizes(size_spec, first_index, n):
@@ -84,25 +181,54 @@ def batch_sizes(size_spec, first_index, n):
     return np.full(n, size_spec, dtype=np.uint32)
 
 
-def main():
-    args = parse()
+def time_steps(torch, device, stream, step, steps, warmup, world, dist):
+    for _ in range(warmup):
+        step()
+    _sync(torch, device)
+    if world > 1:
+        dist.barrier()
+    _sync(torch, device)
+    tm = _Timer(torch, device, stream, steps)
+    t0 = time.perf_counter()
+    tm.mark(0)
+    for k in range(steps):
+        step()
+        tm.mark(k + 1)
+    _sync(torch, device)
+    if world > 1:
+        dist.barrier()
+    _sync(torch, device)
+    wall = time.perf_counter() - t0
+    kern_ms = [tm.ms(k) for k in range(steps)]
+    return wall / steps, float(np.mean(kern_ms)) / 1e3
+
+
+def rank_main(args, codec_factory=None):
+    """One rank of the benchmark.  `codec_factory(local_rank)` replaces the HIP
+    codec only in the CPU launcher test (tests/test_distributed.py)."""
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = args.device == "cuda"
+    if gpu:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    codec = fsg.SnappyGPU(local)
+        dist.init_process_group("nccl" if gpu else "gloo", init_method="env://")
+        world = dist.get_world_size()
+    codec = codec_factory(local) if codec_factory else fsg.SnappyGPU(local)
     codec.select_kernels(args.decode_kernel, args.encode_kernel)
 
-    op, kind, n_default, size_spec, desc = WORKLOADS[args.workload]
+    op, kind, n_default, size_spec, scaling_default, desc = WORKLOADS[args.workload]
+    scaling = args.scaling or scaling_default
     n_cfg = args.n_msgs or n_default
     t_gen = time.time()
-    if args.scaling == "weak":
+    if scaling == "weak":
         first, last = shard.weak_range(n_cfg, rank)  # rank owns [rank*n, (rank+1)*n)
     else:
         first, last = shard.byte_balanced_ranges(batch_sizes(size_spec, 0, n_cfg), world)[rank]
@@ -113,27 +239,28 @@ def main():
     def H(a):
         return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
+    stream = torch.cuda.current_stream(dev) if gpu else None
     d_raw = H(batch.data)
     d_raw_off, d_raw_len = H(batch.offsets), H(batch.lens)
     caps = np.array([fsg.max_compressed_length(int(x)) for x in batch.lens], dtype=np.uint64)
     c_off, c_tot = fsg.slot_offsets(caps)
     d_comp = torch.zeros(c_tot, dtype=torch.uint8, device=dev)
     d_comp_off = H(c_off)
-    d_comp_len = torch.zeros(n, dtype=torch.int32, device=dev)
-    d_status = torch.zeros(n, dtype=torch.int32, device=dev)
-    max_len = int(batch.lens.max())
+    d_comp_len = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+    d_status = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+    max_len = int(batch.lens.max()) if n else 0
     d_ws = codec.compress_workspace(n, max_len)
     # Compressed inputs come from the GPU encoder (checked against the oracle below).
     codec.compress(d_raw, d_raw_off, d_raw_len, n, max_len, d_comp, d_comp_off, d_comp_len, d_status,
-                   workspace=d_ws)
-    torch.cuda.synchronize()
-    comp_len = d_comp_len.cpu().numpy().view(np.uint32).copy()
+                   stream=stream, workspace=d_ws)
+    _sync(torch, dev)
+    comp_len = d_comp_len.cpu().numpy()[:n].view(np.uint32).copy()
     comp_total = int(comp_len.astype(np.uint64).sum())
-    errors = int((d_status != 0).sum().item())
+    errors = int((d_status[:n] != 0).sum().item())
 
     # Oracle spot check of the compressed bytes (checker only, never timed).
     sample_ok = None
-    if args.verify_sample > 0:
+    if args.verify_sample > 0 and n:
         sys.path.insert(0, str(REPO / "oracle"))
         from bind import Oracle
         orc = Oracle()
@@ -145,53 +272,41 @@ def main():
 
     # Decode output slots (exact uncompressed sizes) -- laid out like the raw batch.
     d_out = torch.zeros(max(raw_total, 1), dtype=torch.uint8, device=dev)
-    d_out_len = torch.zeros(n, dtype=torch.int32, device=dev)
-    d_cap = d_raw_len
-    d_comp_len_u = d_comp_len  # int32 view is fine: lengths < 2^31
-    stream = torch.cuda.current_stream()
+    d_out_len = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
     d_dws = codec.decompress_workspace(n, c_tot)
 
-    if op == "decompress":
-        def step():
-            codec.decompress(d_comp, d_comp_off, d_comp_len_u, n, d_out, d_raw_off, d_cap, d_out_len,
-                             d_status, stream=stream, workspace=d_dws)
-        algo_bytes = raw_total + comp_total  # each input byte read once, each output byte written once
-    else:
-        def step():
-            codec.compress(d_raw, d_raw_off, d_raw_len, n, max_len, d_comp, d_comp_off, d_comp_len,
-                           d_status, stream=stream, workspace=d_ws)
-        algo_bytes = raw_total + comp_total
+    def decode_step():
+        codec.decompress(d_comp, d_comp_off, d_comp_len, n, d_out, d_raw_off, d_raw_len, d_out_len,
+                         d_status, stream=stream, workspace=d_dws)
+
+    def encode_step():
+        codec.compress(d_raw, d_raw_off, d_raw_len, n, max_len, d_comp, d_comp_off, d_comp_len,
+                       d_status, stream=stream, workspace=d_ws)
+
+    step = decode_step if op == "decompress" else encode_step
+    algo_bytes = raw_total + comp_total  # each input byte read once, each output byte written once
     gen_s = time.time() - t_gen
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-    t0 = time.perf_counter()
-    evs[0].record(stream)
-    for k in range(args.steps):
-        step()
-        evs[k + 1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kern_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)]
-    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+    t_step, avg_kernel_s = time_steps(torch, dev, stream, step, args.steps, args.warmup, world, dist)
 
     # Correctness of the timed output (device-side, untimed).
+    errors += int((d_status[:n] != 0).sum().item())
     if op == "decompress":
-        errors += int((d_status != 0).sum().item())
         roundtrip_ok = bool(torch.equal(d_out[:raw_total], d_raw[:raw_total]))
     else:
-        errors += int((d_status != 0).sum().item())
-        roundtrip_ok = bool((d_comp_len.cpu().numpy().view(np.uint32) == comp_len).all())
+        roundtrip_ok = bool((d_comp_len.cpu().numpy()[:n].view(np.uint32) == comp_len).all())
 
-    t_step = wall / args.steps
+    # Per-message (out_len, status) of every rank, gathered over RCCL.
+    gather = gather_results(torch, dist, dev, world, rank, n, d_out_len, d_status,
+                            batch.lens if op == "decompress" else comp_len) if world > 1 else None
+
+    # Root-scatter variant: rank 0 is the only ingress; it sends each peer a
+    # compressed shard with grouped send/recv, then every rank decodes.
+    rscatter = None
+    if world > 1 and op == "decompress" and not args.no_root_scatter:
+        rscatter = root_scatter(torch, dist, dev, stream, world, rank, codec, d_comp, d_comp_off,
+                                d_comp_len, n, d_raw, d_raw_len, d_raw_off, raw_total, c_tot)
+
     if world > 1:
         t_step, avg_kernel_s, (raw_all, comp_all, errors, bad) = shard.reduce_measurements(
             dist, dev, t_step, avg_kernel_s, raw_total, comp_total, errors, int(not roundtrip_ok))
@@ -199,9 +314,15 @@ def main():
     else:
         raw_all, comp_all = raw_total, comp_total
 
+    # The encode leg of the default decode run (same bodies, already resident).
+    enc = None
+    if op == "decompress" and not args.no_encode and args.workload == "c3-decompress" and world == 1:
+        enc = encode_leg(torch, dev, stream, encode_step, d_comp, d_comp_len, comp_len, raw_total,
+                         comp_total, args, batch, c_off)
+
     # End-to-end (host pinned -> device -> kernel -> host pinned), untimed in `value`.
     e2e = None
-    if not args.no_e2e and rank == 0:
+    if not args.no_e2e and rank == 0 and gpu:
         e2e = end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp_total, n,
                          max_len, dev, d_ws)
 
@@ -212,9 +333,10 @@ def main():
     if rank == 0:
         value = raw_all / t_step / GIB
         achieved = algo_bytes / avg_kernel_s / 1e9
-        pmc = load_traffic(args.workload)
+        # PMC traffic is per launch of the full-size workload on one rank's shard
+        pmc = load_traffic(args.workload) if (args.n_msgs == 0 and scaling == "weak") else None
         line = {
-            "metric": "GiB/s device-resident Snappy decode+encode, batched RPC bodies, 1/2/4/8 GPU",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "GiB/s (uncompressed bytes)",
             "n_gpus": world,
@@ -222,7 +344,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(t_step * 1e3, 4),
             "higher_is_better": True,
-            "scaling": args.scaling,
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64-seeded bodies, SURVEY.md §8(d)); compressed by the GPU "
@@ -230,13 +352,15 @@ def main():
             "config": {
                 "workload": desc,
                 "op": op,
-                "messages_per_gpu": n,
-                "global_batch": n * world if args.scaling == "weak" else n_cfg,
-                "raw_bytes_per_gpu": raw_total,
-                "compressed_bytes_per_gpu": comp_total,
-                "ratio": round(raw_total / max(1, comp_total), 4),
-                "parallelism": f"shard{world} ({args.scaling}: messages by index"
-                               f"{', byte-balanced' if args.scaling == 'strong' else ''}; no data-path collective)",
+                "messages_rank0": n,
+                "global_batch": n * world if scaling == "weak" else n_cfg,
+                "raw_bytes_all_ranks": raw_all,
+                "compressed_bytes_all_ranks": comp_all,
+                "ratio": round(raw_all / max(1, comp_all), 4),
+                "parallelism": f"shard{world} ({scaling}: messages by index"
+                               f"{', byte-balanced' if scaling == 'strong' else ''}; no data-path collective)",
+                "world_size_seen_by_collectives": world,
+                "backend": ("nccl (RCCL over xGMI)" if gpu else "gloo") if world > 1 else None,
             },
             "roofline": {
                 "bound": "hbm",
@@ -249,18 +373,140 @@ def main():
                 "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
                 "read_frac": round((comp_total if op == "decompress" else raw_total) / avg_kernel_s / 1e9
                                    / HBM_PEAK_GBS, 4),
+                "note": "rank 0's bytes / MAX over ranks of the HIP-event launch time" if world > 1 else
+                        "algorithmic bytes / average HIP-event duration of one launch on its stream",
             },
             "cpu_baseline": cpu,
+            "encode": enc,
             "end_to_end": e2e,
+            "multi_gpu": {"allgather": gather, "root_scatter": rscatter} if world > 1 else None,
             "correct": {"status_errors": errors, "roundtrip_ok": roundtrip_ok, "oracle_sample_ok": sample_ok},
             "kernel_src": kernel_source_hash(),
-            "decode_lanes": args.decode_lanes,
             "kernels": {"decode": args.decode_kernel, "encode": args.encode_kernel},
             "setup_s": round(gen_s, 2),
         }
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def gather_results(torch, dist, dev, world, rank, n, d_out_len, d_status, expect_len):
+    """ncclAllGather of per-message (out_len, status): every rank ends with the
+    whole batch's results.  Ranks hold different counts under strong scaling,
+    so the rows are padded to the largest shard."""
+    counts = torch.tensor([n], dtype=torch.int64, device=dev)
+    allc = [torch.zeros_like(counts) for _ in range(world)]
+    dist.all_gather(allc, counts)
+    ns = [int(c.item()) for c in allc]
+    mx = max(ns)
+    mine = torch.full((mx, 2), -1, dtype=torch.int32, device=dev)
+    if n:
+        mine[:n, 0] = d_out_len[:n]
+        mine[:n, 1] = d_status[:n]
+    rows = [torch.empty_like(mine) for _ in range(world)]
+    _sync(torch, dev)
+    t0 = time.perf_counter()
+    dist.all_gather(rows, mine)
+    _sync(torch, dev)
+    ms = (time.perf_counter() - t0) * 1e3
+    both = torch.cat([r[:k] for r, k in zip(rows, ns)]).cpu().numpy()
+    # each rank checks its own rows against its expected lengths; SUM the mismatches
+    own = both[sum(ns[:rank]):sum(ns[:rank]) + n]
+    bad = int((own[:, 1] != 0).sum()) + int(
+        (own[:, 0].astype(np.int64) != np.asarray(expect_len[:n]).astype(np.int64)).sum())
+    t = torch.tensor([bad], dtype=torch.int64, device=dev)
+    dist.all_reduce(t)
+    return {"messages": int(both.shape[0]), "bytes_per_rank": mx * 8, "ms": round(ms, 3),
+            "mismatches": int(t.item()),
+            "note": "all_gather of per-message (out_len:u32, status:i32) over all ranks"}
+
+
+def root_scatter(torch, dist, dev, stream, world, rank, codec, d_comp, d_comp_off, d_comp_len, n,
+                 d_raw, d_raw_len, d_raw_off, raw_total, c_tot):
+    """One ingress, N decoders: rank 0 holds every rank's compressed shard (the
+    ranks hand them over first, untimed) and sends each to its rank with
+    grouped send/recv (RCCL has no scatterv); then every rank decodes its shard
+    and checks the output against its own bodies.  Reported beside the
+    pre-placed rate, never as `value`."""
+    sizes = torch.tensor([c_tot], dtype=torch.int64, device=dev)
+    alls = [torch.zeros_like(sizes) for _ in range(world)]
+    dist.all_gather(alls, sizes)
+    nb = [int(x.item()) for x in alls]
+    ingress = None
+    if rank == 0:  # untimed: collect the shards at the ingress rank
+        ingress = [d_comp[:nb[0]]] + [torch.empty(nb[r], dtype=torch.uint8, device=dev) for r in range(1, world)]
+        ops = [dist.P2POp(dist.irecv, ingress[r], r) for r in range(1, world)]
+    else:
+        ops = [dist.P2POp(dist.isend, d_comp[:c_tot], 0)]
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    _sync(torch, dev)
+    recv = d_comp if rank == 0 else torch.empty(c_tot, dtype=torch.uint8, device=dev)
+    out = torch.empty(max(raw_total, 1), dtype=torch.uint8, device=dev)
+    ol = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    st = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    ws = codec.decompress_workspace(n, c_tot)
+    best = None
+    for _ in range(2):
+        if rank != 0:
+            recv.zero_()
+        _sync(torch, dev)
+        dist.barrier()
+        _sync(torch, dev)
+        t0 = time.perf_counter()
+        if rank == 0:
+            ops = [dist.P2POp(dist.isend, ingress[r], r) for r in range(1, world)]
+        else:
+            ops = [dist.P2POp(dist.irecv, recv, 0)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        _sync(torch, dev)
+        t_sc = time.perf_counter() - t0
+        codec.decompress(recv, d_comp_off, d_comp_len, n, out, d_raw_off, d_raw_len, ol, st, stream=stream,
+                         workspace=ws)
+        _sync(torch, dev)
+        t = torch.tensor([t_sc, time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if best is None or float(t[1]) < best[1]:
+            best = (float(t[0]), float(t[1]))
+    bad = int((st[:n] != 0).sum().item()) + int(not torch.equal(out[:raw_total], d_raw[:raw_total]))
+    cnt = torch.tensor([bad, raw_total], dtype=torch.int64, device=dev)
+    dist.all_reduce(cnt)
+    sent = sum(nb[1:])
+    return {"scatter_ms": round(best[0] * 1e3, 3), "scatter_plus_decode_ms": round(best[1] * 1e3, 3),
+            "root_egress_gb_s": round(sent / best[0] / 1e9, 2),
+            "gib_s_uncompressed_all_ranks": round(int(cnt[1]) / best[1] / GIB, 3),
+            "mismatches": int(cnt[0].item()),
+            "note": "rank 0 holds every compressed shard and sends each to its rank (grouped isend/irecv), "
+                    "then all ranks decode; MAX over ranks; output checked against each rank's bodies"}
+
+
+def encode_leg(torch, dev, stream, encode_step, d_comp, d_comp_len, comp_len, raw_total, comp_total,
+               args, batch, c_off):
+    """C3 compress of the same bodies: the encode half of the metric."""
+    steps = max(3, min(args.steps, 10))
+    t_step, avg_kernel_s = time_steps(torch, dev, stream, encode_step, steps, 1, 1, None)
+    ok = bool((d_comp_len.cpu().numpy()[:len(comp_len)].view(np.uint32) == comp_len).all())
+    achieved = (raw_total + comp_total) / avg_kernel_s / 1e9
+    pmc = load_traffic("c3-compress")
+    out = {
+        "workload": "C3 compress: the same 65,536 x 64 KiB bodies, device-resident",
+        "value": round(raw_total / t_step / GIB, 3),
+        "unit": "GiB/s (uncompressed bytes)",
+        "steps": steps,
+        "ms_per_step": round(t_step * 1e3, 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": pmc.get("traffic_bytes_per_launch") if pmc else None,
+                     "algorithmic_bytes_per_launch": raw_total + comp_total,
+                     "avg_kernel_ms": round(avg_kernel_s * 1e3, 4)},
+        "lengths_match_first_encode": ok,
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline("compress", batch, d_comp, c_off, comp_len, args.cpu_threads,
+                                           with_single=False)
+    return out
 
 
 def load_traffic(workload: str):
@@ -278,7 +524,7 @@ def end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp
     d_dws = codec.decompress_workspace(n, d_comp.numel())
     if op == "decompress":
         h_in = torch.empty(d_comp.numel(), dtype=torch.uint8, pin_memory=True)
-        h_in.copy_(d_comp.cpu())
+        h_in.copy_(d_comp)  # device -> pinned, so the pages are touched before the timed H2D
         h_out = torch.empty(raw_total, dtype=torch.uint8, pin_memory=True)
         d_in = torch.empty_like(d_comp)
         d_out = torch.empty(raw_total, dtype=torch.uint8, device=dev)
@@ -386,59 +632,104 @@ def end_to_end_pipelined(torch, codec, h_in, h_out, d_in, d_out, c_off, comp_len
                     "dependencies"}
 
 
-def cpu_baseline(op, batch, d_comp, c_off, comp_len, threads):
+def _cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(op, batch, d_comp, c_off, comp_len, threads, with_single=True):
     """The reference's own CPU Snappy (oracle/_ref, per-message Source/Sink path with
     8160-byte cord_buf fragments) on a bounded sample of the same workload, timed on
-    this host's cores.  Falls back to the C restatement ("port") if _ref is absent."""
+    this host's cores: `threads` (default: the box's share, at most 16), plus a
+    1-thread and an nproc-thread figure.  Falls back to the C restatement ("port")
+    if _ref is absent."""
     sys.path.insert(0, str(REPO / "oracle"))
     from bind import Oracle, Reference
-    nthreads = threads or max(1, min(16, len(os.sched_getaffinity(0))))
+    affinity = len(os.sched_getaffinity(0))
+    nproc = os.cpu_count() or affinity
+    nthreads = threads or max(1, min(16, affinity))
     n = len(batch)
     per_msg = batch.total / max(1, n)
-    # bounded sample: ~1 GiB of decode work or ~0.25 GiB of encode work per pass
-    target = (1 << 30) if op == "decompress" else (1 << 28)
-    m = int(max(1, min(n, target // max(1, per_msg))))
-    lens = batch.lens[:m].copy()
-    offs = batch.offsets[:m].copy()
-    host_comp = d_comp[: int(c_off[m - 1] + comp_len[m - 1]) + 1].cpu().numpy()
-    clen = comp_len[:m].copy()
-    coff = c_off[:m].copy()
     kind = "reference" if Reference.available() else "port"
     eng = Reference() if kind == "reference" else Oracle()
-    out_len = np.zeros(m, np.uint32)
-    # repeated passes over the sample until ~1 s of wall time (~16 s of CPU
-    # work at 16 threads), at most 20 passes
-    passes, dt = 0, 0.0
-    while passes < 20 and (passes == 0 or dt < 1.0):
-        if op == "decompress":
-            out = np.zeros(max(1, int(lens.astype(np.uint64).sum())), np.uint8)
-            if kind == "reference":
-                dt += eng.batch(1, host_comp, coff, clen, out, offs, lens, out_len, nthreads)
+    host_all = None
+
+    def run(nthr, target_bytes, min_wall):
+        nonlocal host_all
+        m = int(max(1, min(n, target_bytes // max(1, per_msg))))
+        lens = batch.lens[:m].copy()
+        offs = batch.offsets[:m].copy()
+        if host_all is None:
+            host_all = d_comp.cpu().numpy()
+        host_comp = host_all[: int(c_off[m - 1] + comp_len[m - 1]) + 1]
+        clen = comp_len[:m].copy()
+        coff = c_off[:m].copy()
+        out_len = np.zeros(m, np.uint32)
+        passes, dt, ok = 0, 0.0, True
+        while passes < 20 and (passes == 0 or dt < min_wall):
+            if op == "decompress":
+                out = np.zeros(max(1, int(lens.astype(np.uint64).sum())), np.uint8)
+                if kind == "reference":
+                    dt += eng.batch(1, host_comp, coff, clen, out, offs, lens, out_len, nthr)
+                else:
+                    st = np.zeros(m, np.int32)
+                    dt += eng.uncompress_batch(host_comp, coff, clen, out, offs, lens, out_len, st, nthr)
+                nraw = int(lens.astype(np.uint64).sum())
+                ok = ok and bool(np.array_equal(out[:nraw], batch.data[:nraw]))
             else:
-                st = np.zeros(m, np.int32)
-                dt += eng.uncompress_batch(host_comp, coff, clen, out, offs, lens, out_len, st, nthreads)
-            nraw = int(lens.astype(np.uint64).sum())
-            ok = bool(np.array_equal(out[:nraw], batch.data[:nraw]))
-        else:
-            caps = np.array([fsg.max_compressed_length(int(x)) for x in lens], np.uint64)
-            oo, tot = fsg.slot_offsets(caps)
-            out = np.zeros(tot, np.uint8)
-            if kind == "reference":
-                dt += eng.batch(0, batch.data, offs, lens, out, oo, None, out_len, nthreads)
-            else:
-                dt += eng.compress_batch(batch.data, offs, lens, out, oo, out_len, nthreads)
-            ok = bool(np.array_equal(out_len, clen))
-        passes += 1
-    raw = int(lens.astype(np.uint64).sum()) * passes
-    return {
-        "value": round(raw / dt / GIB, 3),
+                caps = np.array([fsg.max_compressed_length(int(x)) for x in lens], np.uint64)
+                oo, tot = fsg.slot_offsets(caps)
+                out = np.zeros(tot, np.uint8)
+                if kind == "reference":
+                    dt += eng.batch(0, batch.data, offs, lens, out, oo, None, out_len, nthr)
+                else:
+                    dt += eng.compress_batch(batch.data, offs, lens, out, oo, out_len, nthr)
+                ok = ok and bool(np.array_equal(out_len, clen))
+            passes += 1
+        raw = int(lens.astype(np.uint64).sum()) * passes
+        return raw / dt / GIB, m, raw / passes, passes, dt, ok
+
+    # bounded sample: ~1 GiB of decode work or ~0.25 GiB of encode work per pass
+    target = (1 << 30) if op == "decompress" else (1 << 28)
+    v, m, raw1, passes, dt, ok = run(nthreads, target, 1.0)
+    res = {
+        "value": round(v, 3),
         "unit": "GiB/s (uncompressed bytes)",
         "cores": nthreads,
         "kind": kind,
-        "sample": f"first {m} messages of the same batch ({raw / passes / GIB:.3f} GiB raw) x {passes} "
+        "sample": f"first {m} messages of the same batch ({raw1 / GIB:.3f} GiB raw) x {passes} "
                   f"passes, {op}, {nthreads} threads x strided messages, 8160-B fragments; wall {dt:.3f} s "
                   f"(~{dt * nthreads:.0f} s of CPU work); output equal to GPU's: {ok}",
+        "host": {"cpu_model": _cpu_model(), "nproc": nproc, "affinity_cpus": affinity},
     }
+    if with_single:
+        v1, m1, raw_s, p1, dt1, ok1 = run(1, target // 16, 1.0)
+        res["single_thread"] = {"value": round(v1, 3), "cores": 1,
+                                "sample": f"first {m1} messages ({raw_s / GIB:.3f} GiB raw) x {p1} passes, "
+                                          f"wall {dt1:.3f} s; output equal: {ok1}"}
+        if affinity > nthreads:
+            vn, mn, raw_n, pn, dtn, okn = run(affinity, target, 0.5)
+            res["all_cpus"] = {"value": round(vn, 3), "cores": affinity,
+                               "sample": f"first {mn} messages ({raw_n / GIB:.3f} GiB raw) x {pn} passes, "
+                                         f"wall {dtn:.3f} s; output equal: {okn}"}
+    return res
+
+
+def main(argv=None):
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launcher: spawn the ranks before this process touches the GPU
+        sys.exit(launch(args.gpus, sys.argv[1:] if argv is None else list(argv)))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world and "WORLD_SIZE" in os.environ:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} ranks",
+              file=sys.stderr)
+    rank_main(args)
 
 
 if __name__ == "__main__":

@@ -1074,8 +1074,10 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     // then one wave per message
     const u32 small_blocks = (n_msgs + kWavesPerBlock - 1) / kWavesPerBlock;
     static const u32 kBigBlocks = [] {  // A/B knob
+      // at least one block: the large-message lists are only drained there
       const char* e = getenv("FSG_EXEC_BIG_BLOCKS");
-      return e ? (u32)atoi(e) : 512u;
+      const int v = e ? atoi(e) : 512;
+      return v >= 1 ? (u32)v : 512u;
     }();
     const u32 big_blocks = small_blocks < kBigBlocks ? small_blocks : kBigBlocks;
     exec_kernel<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(

@@ -119,11 +119,17 @@ int cord_buf::append(const void* data, size_t n) {
 }
 
 void cord_buf::append(const cord_buf& other) {
-  for (const Ref& r : other.refs_) {
+  // snapshot the count and index by position: `other` may be *this, whose
+  // vector reallocates as it grows (the reference's append(self) works too)
+  const size_t nrefs = other.refs_.size();
+  const size_t nbytes = other.size_;
+  refs_.reserve(refs_.size() + nrefs);
+  for (size_t i = 0; i < nrefs; ++i) {
+    const Ref r = other.refs_[i];
     inc_ref(r.block);
     refs_.push_back(r);
   }
-  size_ += other.size_;
+  size_ += nbytes;
 }
 
 int cord_buf::append_user_data(void* data, size_t size, void (*deleter)(void*)) {

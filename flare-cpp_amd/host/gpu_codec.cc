@@ -178,7 +178,9 @@ void SnappyGpuCodec::Impl::run(const std::vector<Request*>& reqs, bool compress)
   uint32_t max_len = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const size_t len = reqs[i]->in->size();
-    if (len > 0xffffffffu) {  // beyond the format's uint32 lengths
+    // beyond the format's uint32 lengths, or (compress) a worst-case output
+    // the u32 slot sizes cannot describe
+    if (len > 0xffffffffu || (compress && fsg_max_compressed_length(len) > 0xffffffffu)) {
       skip[i] = 1;
       continue;
     }

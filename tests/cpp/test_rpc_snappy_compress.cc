@@ -123,6 +123,18 @@ TEST_CPU(cord_buf_blocks) {
   ASSERT_EQ(freed.load(), 1);
 }
 
+TEST_CPU(cord_buf_append_self) {
+  // the reference's append(const cord_buf&) works when other == *this
+  cord_buf b;
+  std::string s = pattern(30000, true);  // 4 refs: the append below reallocates
+  b.append(s);
+  b.append(b);
+  ASSERT_EQ(b.size(), 2 * s.size());
+  ASSERT_EQ(b.to_string(), s + s);
+  b.append(b);
+  ASSERT_EQ(b.to_string(), s + s + s + s);
+}
+
 TEST_CPU(cord_buf_blockmem_hook) {
   static std::atomic<int> allocs{0};
   void* (*old_a)(size_t) = flare::iobuf::blockmem_allocate;

@@ -77,3 +77,48 @@ def test_two_rank_gloo_shards_reassemble():
     merged = [d for lo, ds in sorted(gathered) for d in ds]
     assert merged == whole
     assert cb == sum(len(o.compress(b.item(i))) for i in range(len(b)))
+
+
+def _run_bench_launcher(nprocs, extra):
+    """bench.py's own launcher (bench.launch) starting CPU ranks whose codec is
+    the oracle (tests/bench_cpu_rank.py); returns rank 0's JSON line."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parents[1]
+    argv = ["--device", "cpu", "--gpus", str(nprocs), "--steps", "2", "--warmup", "1", "--no-e2e",
+            "--no-cpu-baseline", "--verify-sample", "4", *extra]
+    code = ("import sys; sys.path.insert(0, %r); import bench; "
+            "sys.exit(bench.launch(%d, %r, entry=%r, timeout_s=240))"
+            % (str(repo), nprocs, argv, str(repo / "tests" / "bench_cpu_rank.py")))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 prints ONE line
+    return json.loads(lines[0])
+
+
+def test_bench_launcher_two_ranks_weak():
+    d = _run_bench_launcher(2, ["--workload", "c3-decompress", "--n-msgs", "48"])
+    assert d["n_gpus"] == 2 and d["config"]["world_size_seen_by_collectives"] == 2
+    assert d["scaling"] == "weak" and d["config"]["global_batch"] == 96
+    assert d["config"]["raw_bytes_all_ranks"] == 96 * 65536
+    assert d["correct"]["status_errors"] == 0 and d["correct"]["roundtrip_ok"]
+    assert d["correct"]["oracle_sample_ok"]
+    ag = d["multi_gpu"]["allgather"]
+    assert ag["messages"] == 96 and ag["mismatches"] == 0
+    rs = d["multi_gpu"]["root_scatter"]
+    assert rs["mismatches"] == 0 and rs["scatter_plus_decode_ms"] > 0
+
+
+def test_bench_launcher_two_ranks_strong_mixed():
+    d = _run_bench_launcher(2, ["--workload", "cm-decompress", "--n-msgs", "600"])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["global_batch"] == 600
+    sizes = fsg.mixed_sizes(600)
+    assert d["config"]["raw_bytes_all_ranks"] == int(sizes.astype(np.uint64).sum())
+    assert d["correct"]["status_errors"] == 0 and d["correct"]["roundtrip_ok"]
+    assert d["multi_gpu"]["allgather"]["messages"] == 600
+    assert d["multi_gpu"]["allgather"]["mismatches"] == 0
+    assert d["multi_gpu"]["root_scatter"]["mismatches"] == 0
