@@ -318,11 +318,14 @@ __global__ __launch_bounds__(64) void index_kernel(
       const u32 ip_next = look ? nx : ip;
       if (j + 1 < kIdxTags) ring_read(ip_next, lo, hi);
       const u32 coff = val | ((type == 1 ? c >> 5 : 0u) << 8);
-      // tag bytes and literal bytes present (:744-761): the next tag position
-      // is inside the input (nx < ip only when a 4-byte literal length wrapped
-      // it); copy offset in range (:1200, 1410, 1466).  The writer's space
+      // tag bytes and literal bytes present (:744-761), compared against the
+      // bytes left after the tag so no sum can wrap (a 4-byte literal length
+      // of 0xfffffffa..0xfffffffe would wrap nx back onto its own length
+      // bytes); copy offset in range (:1200, 1410, 1466).  The writer's space
       // check (:1166, :1400) is per iteration, below: op only grows.
-      const bool bad = (nx > n_in) | (nx < ip) | ((coff - 1u >= op) & (type != 0));
+      const u32 avail = n_in - ip - 1;  // ip < n_in whenever `look`
+      const bool bad = (avail < nb) | ((avail - nb < len) & (type == 0)) |
+                       ((coff - 1u >= op) & (type != 0));
       status = (look && bad) ? kCorrupt : status;
       const bool take = look && !bad;
       // unconditional (bits land in the LDS ring even without a bitmap): a

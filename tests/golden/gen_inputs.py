@@ -137,6 +137,13 @@ def negative_cases(ref) -> list[tuple[str, bytes]]:
         ("literal_huge", b"\x01\xfc\x00\x00\x00\x80\x00a"),
         ("literal_61", b"\x3d" + b"\xf0\x3c" + bytes(range(61))),
     ]
+    # 4-byte literal lengths 0xfffffffa..0xfffffffe: tag position + 5 + length
+    # wraps back to 0..4 bytes past the tag, so a u32 walk lands on its own
+    # length bytes (0xff = a COPY_4 of 64) and the wrapped op can look sane.
+    for val in range(0xFFFFFFFA, 0xFFFFFFFF):
+        body = b"\x24" + b"0123456789" + b"\xfc" + val.to_bytes(4, "little") + b"\x01\x00\x00\x00"
+        for ulen in (73, 74, 10):
+            cases.append((f"literal_len_wrap_{val:08x}_u{ulen}", _varint(ulen) + body))
     # COPY_4 crossing a 64 KiB block (accepted by the reference decoder): a
     # 70000-byte literal then a COPY_4 with offset 69000 of length 64.
     lit = _rand_bytes(99, 70000)
