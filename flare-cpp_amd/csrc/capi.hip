@@ -14,10 +14,6 @@ hipError_t launch_decode(const u8* in, const u64* in_off, const u32* in_len,
                          u32 n_msgs, u8* out, const u64* out_off,
                          const u32* out_cap, u32* out_len, i32* status,
                          u32 flags, hipStream_t stream);
-hipError_t launch_decode_v2(const u8* in, const u64* in_off, const u32* in_len,
-                            u32 n_msgs, u8* out, const u64* out_off,
-                            const u32* out_cap, u32* out_len, i32* status,
-                            u32 flags, u32* counter, u32 lanes, hipStream_t stream);
 hipError_t launch_decode_v3(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u8* out, const u64* out_off,
                             const u32* out_cap, u32* out_len, i32* status,
@@ -29,11 +25,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
                             u32 flags, void* ws, size_t ws_bytes, hipStream_t stream);
 hipError_t launch_headers(const u8* in, const u64* in_off, const u32* in_len,
                           u32 n_msgs, u32* ulen, int lenient, hipStream_t stream);
-size_t encode_v2_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out);
-hipError_t launch_encode_v2(const u8* in, const u64* in_off, const u32* in_len,
-                            u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
-                            u32* out_len, i32* status, void* ws, size_t ws_bytes,
-                            hipStream_t stream);
+size_t encode_tables_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out);
 size_t encode_plan_bytes(u32 n_msgs, u32 max_in_len);
 hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
@@ -43,6 +35,8 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
 hipError_t launch_encode(const u8* in, const u64* in_off, const u32* in_len,
                          u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                          u32* out_len, i32* status, hipStream_t stream);
+hipError_t launch_gather_blocks(const u64* src, const u32* len, const u64* dst_off, u32 n, u8* dst,
+                                hipStream_t stream);
 }  // namespace fsg
 
 namespace {
@@ -56,10 +50,6 @@ int env_int(const char* name) {
 // FSG_ENCODE_KERNEL, changeable with fsg_select_kernels for A/B runs.
 std::atomic<int> g_decode_variant{env_int("FSG_DECODE_KERNEL")};
 std::atomic<int> g_encode_variant{env_int("FSG_ENCODE_KERNEL")};
-// Lanes in flight for the persistent decoder (0 = one lane per message).
-// Measured on C3: capping lanes below the message count only removes
-// latency hiding (16384 lanes: 35 ms vs 15 ms with one lane per message).
-std::atomic<unsigned> g_decode_lanes{(unsigned)env_int("FSG_DECODE_LANES")};
 // Test knob: cap the staging region of a split message's fragments (bytes;
 // 0 = slot / fragments).  Small caps force the whole-message fallback pass.
 std::atomic<unsigned> g_region_cap{(unsigned)env_int("FSG_TEST_REGION_CAP")};
@@ -77,18 +67,16 @@ const char* fsg_version(void) { return "flare-snappy-gpu 0.1 gfx950"; }
 
 const char* fsg_last_error(void) { return g_err; }
 
-int fsg_set_decode_lanes(uint32_t lanes) {
-  g_decode_lanes.store(lanes);
-  return FSG_SUCCESS;
-}
-
 int fsg_set_split_region_cap(uint32_t bytes) {
   g_region_cap.store(bytes);
   return FSG_SUCCESS;
 }
 
 int fsg_select_kernels(int decode_variant, int encode_variant) {
-  if (decode_variant < 0 || decode_variant > 4 || encode_variant < 0 || encode_variant > 3)
+  // generation 2 (persistent-lane decode, literal lane encode) was retired:
+  // superseded by 3/4 on every workload
+  if (decode_variant < 0 || decode_variant > 4 || decode_variant == 2 || encode_variant < 0 ||
+      encode_variant > 3 || encode_variant == 2)
     return FSG_ERR_INVALID_ARG;
   g_decode_variant.store(decode_variant);
   g_encode_variant.store(encode_variant);
@@ -108,6 +96,13 @@ int fsg_init(int device) {
 }
 
 size_t fsg_max_compressed_length(size_t n) { return 32 + n + n / 6; }
+
+int fsg_gather_blocks(const uint64_t* d_src, const uint32_t* d_len, const uint64_t* d_dst_off,
+                      uint32_t n, uint8_t* d_dst, void* stream) {
+  if (n && (!d_src || !d_len || !d_dst_off || !d_dst)) return FSG_ERR_INVALID_ARG;
+  return record(fsg::launch_gather_blocks(d_src, d_len, d_dst_off, n, d_dst, (hipStream_t)stream),
+                "fsg_gather_blocks");
+}
 
 int fsg_get_uncompressed_length(const void* compressed, size_t n,
                                 uint32_t* ulen, int lenient) {
@@ -138,7 +133,7 @@ int fsg_uncompressed_lengths_batch(const uint8_t* d_in, const uint64_t* d_in_off
 
 size_t fsg_compress_workspace_bytes(uint32_t n_msgs, uint32_t max_in_len) {
   // per-lane hash tables, then the fragment plan for messages > 64 KiB
-  return fsg::encode_v2_workspace_bytes(n_msgs, max_in_len, nullptr) +
+  return fsg::encode_tables_workspace_bytes(n_msgs, max_in_len, nullptr) +
          fsg::encode_plan_bytes(n_msgs, max_in_len);
 }
 size_t fsg_decompress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_bytes) {
@@ -155,12 +150,12 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
   if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off ||
                  !d_out_len || !d_status))
     return FSG_ERR_INVALID_ARG;
-  // Lane-per-message encoders with global-memory tables when the workspace
-  // allows it (v3: batched speculative probes, the default; v2: literal
-  // restatement); otherwise the wave-per-message LDS-table encoder (v1).
+  // The lane-per-message encoder with global-memory tables when the
+  // workspace allows it (v3: batched speculative probes, the default);
+  // otherwise the wave-per-message LDS-table encoder (v1).
   const int forced = g_encode_variant.load(std::memory_order_relaxed);
   fsg::u32 slots = 0;
-  const size_t need = fsg::encode_v2_workspace_bytes(n_msgs, max_in_len, &slots);
+  const size_t need = fsg::encode_tables_workspace_bytes(n_msgs, max_in_len, &slots);
   if ((forced == 0 || forced == 3) && d_workspace && workspace_bytes >= need) {
     const fsg::u32 cap = max_in_len == 0 || max_in_len > fsg::kBlockSize ? fsg::kBlockSize : max_in_len;
     // Lanes in flight (tuning knob): fewer lanes keep their tables and
@@ -174,11 +169,6 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
                                         (hipStream_t)stream),
                   "fsg_compress_batch");
   }
-  if (forced == 2 && d_workspace && workspace_bytes >= need)
-    return record(fsg::launch_encode_v2(d_in, d_in_off, d_in_len, n_msgs, max_in_len, d_out,
-                                        d_out_off, d_out_len, d_status, d_workspace,
-                                        workspace_bytes, (hipStream_t)stream),
-                  "fsg_compress_batch");
   return record(fsg::launch_encode(d_in, d_in_off, d_in_len, n_msgs, max_in_len,
                                    d_out, d_out_off, d_out_len, d_status,
                                    (hipStream_t)stream),
@@ -215,18 +205,8 @@ int fsg_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
                                         workspace_bytes, (hipStream_t)stream),
                   "fsg_decompress_batch");
   }
-  if (forced == 0 || forced == 3 || forced == 4)
-    return record(fsg::launch_decode_v3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
-                                        d_out_cap, d_out_len, d_status, flags,
-                                        (hipStream_t)stream),
-                  "fsg_decompress_batch");
-  // v2: persistent decode with a bounded number of lanes in flight when the
-  // workspace (a work counter) is provided.
-  fsg::u32* counter = (d_workspace && workspace_bytes >= 4) ? static_cast<fsg::u32*>(d_workspace) : nullptr;
-  return record(fsg::launch_decode_v2(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
-                                      d_out_cap, d_out_len, d_status, flags, counter,
-                                      g_decode_lanes.load(std::memory_order_relaxed),
-                                      (hipStream_t)stream),
+  return record(fsg::launch_decode_v3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
+                                      d_out_cap, d_out_len, d_status, flags, (hipStream_t)stream),
                 "fsg_decompress_batch");
 }
 

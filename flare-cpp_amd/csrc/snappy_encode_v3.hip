@@ -508,6 +508,20 @@ __global__ __launch_bounds__(256) void encode_gather_kernel(
 
 // Plan region after the tables: items (2 x u32 per fragment), per-item
 // sizes, per-message first item, split-message list.
+// Per-lane hash tables for the lane-per-message encoder: [counter: 256 B]
+// [tables: slots x entries x u16], entries per WorkingMemory::GetHashTable
+// (snappy.cc:247-271) for the largest fragment of the batch.
+size_t encode_tables_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out) {
+  u32 cap = max_in_len == 0 || max_in_len > kBlockSize ? kBlockSize : max_in_len;
+  const u32 entries = table_size_for(cap);
+  // enough lanes to fill the chip several times over: 256 CUs x 16 waves x 64
+  u32 slots = n_msgs < 262144u ? n_msgs : 262144u;
+  slots = (slots + 255) / 256 * 256;
+  if (slots == 0) slots = 256;
+  if (slots_out) *slots_out = slots;
+  return 256 + (size_t)slots * entries * sizeof(u16);
+}
+
 size_t encode_plan_bytes(u32 n_msgs, u32 max_in_len) {
   if (max_in_len <= kBlockSize) return 0;  // (0 = unknown bound: messages are not split)
   const u64 per_msg = (max_in_len + kBlockSize - 1) >> kBlockLog;

@@ -3,12 +3,17 @@
 // second call site of the hot path, public_pbrpc's direct
 // flare::snappy::Compress(const char*, size_t, std::string*)
 // (/root/reference/flare/rpc/policy/public_pbrpc_protocol.cc:137-142).
-// Every call is one (batched) GPU job; bytes are identical to the reference.
+// Large calls are (batched) GPU jobs, small ones run the host codec; bytes
+// and verdicts are identical to the reference.
 #pragma once
 
 #include <cstddef>
 #include <cstdint>
 #include <string>
+
+#include "cord_buf.h"
+
+struct iovec;
 
 namespace flare::snappy {
 
@@ -32,7 +37,19 @@ bool RawUncompress(const char* compressed, size_t compressed_length, char* uncom
 // snappy.cc:235-244 (strict header).
 bool GetUncompressedLength(const char* compressed, size_t compressed_length, size_t* result);
 
-// snappy.cc:1290-1294.
+// snappy.cc:1290-1294 (the device's validate-only pass for large inputs).
 bool IsValidCompressedBuffer(const char* compressed, size_t compressed_length);
+
+// snappy.h:152-164, snappy.cc:1124-1139 (SnappyIOVecWriter): decodes into
+// the iovecs in order; false if the stream is invalid or the iovecs hold
+// fewer bytes than the header length (what they hold then is unspecified).
+bool RawUncompressToIOVec(const char* compressed, size_t compressed_length, const struct iovec* iov,
+                          size_t iov_cnt);
+
+// snappy.h:181-190, snappy.cc:1530-1535: appends what the reference's
+// scattered writer would have produced before the first failing tag, and
+// returns the reference's result (see snappy_cpu.h for its one quirk).
+// Source fragments = the cord_buf's backing blocks.
+size_t UncompressAsMuchAsPossible(const cord_buf& compressed, cord_buf* uncompressed);
 
 }  // namespace flare::snappy

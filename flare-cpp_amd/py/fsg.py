@@ -29,7 +29,6 @@ _SIGS = {
     "fsg_init": (_c.c_int, [_c.c_int]),
     "fsg_last_error": (_c.c_char_p, []),
     "fsg_select_kernels": (_c.c_int, [_c.c_int, _c.c_int]),
-    "fsg_set_decode_lanes": (_c.c_int, [_u32]),
     "fsg_set_split_region_cap": (_c.c_int, [_u32]),
     "fsg_max_compressed_length": (_sz, [_sz]),
     "fsg_get_uncompressed_length": (_c.c_int, [_vp, _sz, _c.POINTER(_u32), _c.c_int]),
@@ -96,9 +95,6 @@ class SnappyGPU:
 
     def set_split_region_cap(self, nbytes: int):
         self._check(self.lib.fsg_set_split_region_cap(nbytes), "fsg_set_split_region_cap")
-
-    def set_decode_lanes(self, lanes: int):
-        self._check(self.lib.fsg_set_decode_lanes(lanes), "fsg_set_decode_lanes")
 
     def compress_workspace(self, n, max_in_len, device=None):
         """Allocate the device workspace fsg_compress_batch wants (torch uint8)."""

@@ -1,9 +1,10 @@
 #!/bin/bash
-# GPU parity suite + the default bench line, each step under its own time limit.
+# GPU parity suite (+ optional default bench line), each step under its own time limit.
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-  > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread \
+  > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
 tail -3 gpurun_out/pytest_gpu.log
+grep -h "latches:\|device batches" gpurun_out/pytest_gpu.log | head -5
 if [ -n "$BENCH_DEFAULT" ]; then
   timeout -k 10 400 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err \
     || { tail -20 gpurun_out/bench_default.err; exit 1; }

@@ -81,22 +81,17 @@ const char *fsg_last_error(void);
 
 /* Kernel variants for A/B measurement and tests: 0 = automatic choice,
  * 1 = first-generation kernels (decode: one lane per message, tag by tag;
- * encode: one wave per message with the hash table in LDS), 2 = second
- * generation (decode: batched pieces, optional persistent lanes; encode: lane
- * per message, tables in the workspace), 3 = third generation (decode:
- * software-pipelined batched pieces; encode: lane per message with batched
- * speculative probes, the default encoder), 4 = decode only: the two-pass
- * decoder (lane-per-message index pass writing a tag-start bitmap, then one
- * wave per message executing <= 16-byte pieces in dependency rounds through an
- * LDS output window), the default decoder whenever the workspace holds its
- * bitmap.  Every variant produces identical bytes and statuses.
- * Process-wide; not for use while other threads launch batches. */
+ * encode: one wave per message with the hash table in LDS), 3 = third
+ * generation (decode: software-pipelined batched pieces, one lane per
+ * message; encode: lane per message with batched speculative probes and the
+ * tables in the workspace, the default encoder), 4 = decode only: the
+ * two-pass decoder (lane-per-message index pass writing a tag-start bitmap,
+ * then one wave per message executing <= 16-byte pieces in dependency rounds
+ * through an LDS output window), the default decoder whenever the workspace
+ * holds its bitmap.  (Generation 2 was retired; 2 is rejected.)  Every
+ * variant produces identical bytes and statuses.  Process-wide; not for use
+ * while other threads launch batches. */
 int fsg_select_kernels(int decode_variant, int encode_variant);
-
-/* Lanes the persistent decoder (decode variant 2) keeps in flight
- * (0 = one per message, the default; or FSG_DECODE_LANES).  Tuning knob;
- * bytes are unaffected. */
-int fsg_set_decode_lanes(uint32_t lanes);
 
 /* Test knob: caps the staging region of each fragment of a message longer
  * than 64 KiB (bytes; 0 = the slot split evenly, the default).  A fragment
@@ -107,6 +102,16 @@ int fsg_set_split_region_cap(uint32_t bytes);
 
 /* 32 + n + n/6 (snappy.cc:55-77). */
 size_t fsg_max_compressed_length(size_t n);
+
+/* Gather: copies n byte ranges (d_src[i], d_len[i]) to d_dst + d_dst_off[i]
+ * on the device.  The sources may be pinned HOST memory (hipHostMalloc'd,
+ * device-mapped): the kernel reads them over PCIe, which is how the host
+ * runtime moves cord_buf blocks from the pinned blockmem_allocate hook
+ * (flare/io/cord_buf.cc:159-166) into a packed batch without a staging
+ * memcpy (the reference walks backing blocks, cord_buf.cc:1469-1475).
+ * d_src / d_len / d_dst_off are device arrays. */
+int fsg_gather_blocks(const uint64_t *d_src, const uint32_t *d_len, const uint64_t *d_dst_off,
+                      uint32_t n, uint8_t *d_dst, void *stream);
 
 /* Host-side header parse.  lenient != 0: ReadUncompressedLength rules
  * (5th byte's high bits dropped); lenient == 0: Parse32WithLimit rules.

@@ -108,6 +108,8 @@ class Reference:
         L.ref_get_uncompressed_length_source.argtypes = [_vp, _sz, _c.POINTER(_u32)]
         L.ref_raw_uncompress.argtypes = [_vp, _sz, _vp]
         L.ref_is_valid.argtypes = [_vp, _sz]
+        L.ref_uncompress_as_much.argtypes = [_vp, _sz, _vp, _sz, _sz, _c.POINTER(_sz)]
+        L.ref_uncompress_as_much.restype = _sz
         L.ref_batch.argtypes = [_c.c_int, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _c.c_int, _sz]
         L.ref_batch.restype = _c.c_double
         self.L = L
@@ -126,6 +128,14 @@ class Reference:
         prod = _sz(0)
         ok = self.L.ref_uncompress(_buf(comp), len(comp), out, cap, ctypes.byref(prod), frag)
         return bool(ok), out.raw[:min(prod.value, cap)]
+
+    def uncompress_as_much(self, comp: bytes, cap: int, frag: int = FRAG):
+        """UncompressAsMuchAsPossible: (its return value, the bytes the sink received)."""
+        out = ctypes.create_string_buffer(max(cap, 1))
+        got = _sz(0)
+        r = self.L.ref_uncompress_as_much(_buf(comp), len(comp), out, cap, frag, ctypes.byref(got))
+        assert got.value <= cap
+        return r, out.raw[:got.value]
 
     def header_source(self, comp: bytes):
         u = _u32(0)

@@ -112,6 +112,16 @@ int ref_get_uncompressed_length(const char* in, size_t n, size_t* ulen) {
 int ref_raw_uncompress(const char* in, size_t n, char* out) {
   return flare::snappy::RawUncompress(in, n, out) ? 1 : 0;
 }
+// snappy::UncompressAsMuchAsPossible(Source*, Sink*) (snappy.cc:1530-1535):
+// returns its result; *got = the bytes the sink received.
+size_t ref_uncompress_as_much(const char* in, size_t n, char* out, size_t cap, size_t frag,
+                              size_t* got) {
+  FragmentSource src(in, n, frag);
+  CopySink sink(out, cap);
+  const size_t r = flare::snappy::UncompressAsMuchAsPossible(&src, &sink);
+  *got = sink.size();
+  return r;
+}
 int ref_is_valid(const char* in, size_t n) {
   return flare::snappy::IsValidCompressedBuffer(in, n) ? 1 : 0;
 }

@@ -4,6 +4,10 @@
 //   ./test_rpc_snappy_compress --cpu   tests that need no GPU
 //   ./test_rpc_snappy_compress --gpu   codec tests (MI355X)
 #include <hip/hip_runtime.h>
+#include <sys/uio.h>
+
+#include <condition_variable>
+#include <mutex>
 
 #include <atomic>
 #include <chrono>
@@ -376,6 +380,216 @@ TEST_GPU(pinned_block_memory) {
   flare::iobuf::blockmem_deallocate = old_d;
 }
 
+// ------------------------------------------------- host runtime (policy) tests
+static std::string flat_compress(const std::string& s) {
+  std::string o;
+  flare::snappy::Compress(s.data(), s.size(), &o);
+  return o;
+}
+
+TEST_CPU(flat_api_on_host_codec) {
+  // no GPU in the CPU run: the flat API runs the host codec; compress never fails
+  const std::string t = pattern(200, true);
+  std::string c;
+  ASSERT_EQ(flare::snappy::Compress(t.data(), t.size(), &c), 49u);
+  ASSERT_EQ(hex(c).substr(0, 6), "c80190");  // known answer
+  std::string back;
+  ASSERT_TRUE(flare::snappy::Uncompress(c.data(), c.size(), &back));
+  ASSERT_EQ(back, t);
+  ASSERT_TRUE(flare::snappy::IsValidCompressedBuffer(c.data(), c.size()));
+  ASSERT_FALSE(flare::snappy::IsValidCompressedBuffer(c.data(), c.size() - 1));
+  cord_buf in, out, b2;
+  in.append(pattern(70000, false));
+  ASSERT_TRUE(policy::SnappyCompress(in, &out));
+  ASSERT_EQ(out.to_string(), flat_compress(in.to_string()));
+  ASSERT_TRUE(policy::SnappyDecompress(out, &b2));
+  ASSERT_TRUE(b2.equals(in.to_string()));
+}
+
+TEST_CPU(iovec_and_as_much_as_possible) {
+  const std::string t = pattern(5000, true);
+  const std::string c = flat_compress(t);
+  char a[1000], b[3000], d[2000];
+  struct iovec iov[3] = {{a, sizeof(a)}, {b, sizeof(b)}, {d, sizeof(d)}};
+  ASSERT_TRUE(flare::snappy::RawUncompressToIOVec(c.data(), c.size(), iov, 3));
+  ASSERT_EQ(std::string(a, 1000) + std::string(b, 3000) + std::string(d, 1000), t);
+  ASSERT_FALSE(flare::snappy::RawUncompressToIOVec(c.data(), c.size(), iov, 2));  // 4000 < 5000
+  // a truncated stream: the scattered writer keeps every complete tag
+  cord_buf in, out;
+  in.append(c.substr(0, c.size() / 2));
+  const size_t r = flare::snappy::UncompressAsMuchAsPossible(in, &out);
+  ASSERT_EQ(r, out.size());
+  ASSERT_TRUE(out.size() > 0 && out.size() < t.size());
+  ASSERT_EQ(out.to_string(), t.substr(0, out.size()));
+}
+
+TEST_GPU(threshold_routes_small_bodies_to_host) {
+  auto& codec = flare::gpu::SnappyGpuCodec::Instance();
+  codec.SetMinGpuBytes(16384);
+  const auto s0 = codec.stats();
+  cord_buf small, big, o1, o2;
+  small.append(pattern(4096, true));
+  big.append(pattern(65536, false));
+  ASSERT_TRUE(policy::SnappyCompress(small, &o1));
+  const auto s1 = codec.stats();
+  ASSERT_TRUE(policy::SnappyCompress(big, &o2));
+  const auto s2 = codec.stats();
+  codec.SetMinGpuBytes(0);
+  ASSERT_EQ(s1.cpu_messages - s0.cpu_messages, 1u);
+  ASSERT_EQ(s1.messages, s0.messages);
+  ASSERT_EQ(s2.messages - s1.messages, 1u);
+  ASSERT_EQ(o1.to_string(), flat_compress(small.to_string()));  // same bytes either way
+  ASSERT_EQ(o2.to_string(), flat_compress(big.to_string()));
+}
+
+TEST_GPU(device_error_falls_back_to_host) {
+  auto& codec = flare::gpu::SnappyGpuCodec::Instance();
+  const auto s0 = codec.stats();
+  cord_buf in, c, back;
+  in.append(pattern(50000, true));
+  flare::gpu::InjectDeviceErrorsForTesting(2);
+  ASSERT_TRUE(policy::SnappyCompress(in, &c));
+  ASSERT_TRUE(policy::SnappyDecompress(c, &back));
+  const auto s1 = codec.stats();
+  ASSERT_EQ(s1.fallbacks - s0.fallbacks, 2u);
+  ASSERT_EQ(c.to_string(), flat_compress(in.to_string()));
+  ASSERT_TRUE(back.equals(in.to_string()));
+  cord_buf bad, o;
+  bad.append(c.to_string().substr(0, c.size() - 7));
+  flare::gpu::InjectDeviceErrorsForTesting(1);
+  ASSERT_FALSE(policy::SnappyDecompress(bad, &o));  // the host codec's verdict is the reference's
+}
+
+TEST_GPU(outputs_adopted_from_pinned_slabs) {
+  auto& codec = flare::gpu::SnappyGpuCodec::Instance();
+  const std::string t = pattern(60000, true);
+  cord_buf in, c;
+  in.append(t);
+  ASSERT_TRUE(policy::SnappyCompress(in, &c));
+  for (int i = 0; i < 300; ++i) {  // slabs go back to the pool as outputs die
+    const auto s0 = codec.stats();
+    cord_buf back;
+    ASSERT_TRUE(policy::SnappyDecompress(c, &back));
+    ASSERT_EQ(codec.stats().adopted - s0.adopted, 1u);
+    ASSERT_EQ(back.backing_block_num(), 1u);
+    std::string_view v = back.backing_block(0);
+    ASSERT_TRUE(flare::gpu::IsPinned(v.data(), v.size()));
+    ASSERT_TRUE(back.equals(t));
+  }
+}
+
+TEST_GPU(pinned_blocks_read_by_the_gpu) {
+  void* (*old_a)(size_t) = flare::iobuf::blockmem_allocate;
+  void (*old_d)(void*) = flare::iobuf::blockmem_deallocate;
+  ASSERT_EQ(flare::gpu::UsePinnedBlocks(), 0);
+  {
+    std::vector<cord_buf> ins(40), cs(40), outs(40);
+    std::vector<const cord_buf*> pin, pcc;
+    std::vector<cord_buf*> pc, po;
+    for (int i = 0; i < 40; ++i) {
+      ins[i].append(pattern(20000 + 3001 * i, i & 1));
+      std::string_view v = ins[i].backing_block(0);
+      ASSERT_TRUE(flare::gpu::IsPinned(v.data(), v.size()));
+      pin.push_back(&ins[i]);
+      pc.push_back(&cs[i]);
+      po.push_back(&outs[i]);
+    }
+    std::vector<bool> ok;
+    auto& codec = flare::gpu::SnappyGpuCodec::Instance();
+    ASSERT_TRUE(codec.CompressBatch(pin, pc, &ok));
+    for (auto* p : pc) pcc.push_back(p);
+    ASSERT_TRUE(codec.UncompressBatch(pcc, po, &ok));
+    for (int i = 0; i < 40; ++i) {
+      ASSERT_EQ(cs[i].to_string(), flat_compress(ins[i].to_string()));
+      ASSERT_TRUE(outs[i].equals(ins[i].to_string()));
+    }
+  }  // every pinned block released before the hooks go back
+  flare::iobuf::blockmem_allocate = old_a;
+  flare::iobuf::blockmem_deallocate = old_d;
+}
+
+namespace {
+struct TestLatch {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool set = false;
+};
+std::atomic<int> g_park[4];
+}  // namespace
+
+TEST_GPU(park_hooks_used_by_followers) {
+  for (auto& x : g_park) x = 0;
+  flare::gpu::ParkHooks h;
+  h.create = [] { ++g_park[0]; return (void*)new TestLatch; };
+  h.wait = [](void* p) {
+    ++g_park[1];
+    auto* l = static_cast<TestLatch*>(p);
+    std::unique_lock<std::mutex> lk(l->mu);
+    l->cv.wait(lk, [&] { return l->set; });
+  };
+  h.signal = [](void* p) {
+    ++g_park[2];
+    auto* l = static_cast<TestLatch*>(p);
+    std::lock_guard<std::mutex> lk(l->mu);
+    l->set = true;
+    l->cv.notify_all();
+  };
+  h.destroy = [](void* p) { ++g_park[3]; delete static_cast<TestLatch*>(p); };
+  auto& codec = flare::gpu::SnappyGpuCodec::Instance();
+  codec.SetParkHooks(h);
+  std::atomic<int> bad{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < 16; ++t)
+    th.emplace_back([t, &bad] {
+      for (int i = 0; i < 40; ++i) {
+        cord_buf in, c, back;
+        in.append(pattern(20000 + 97 * t + i, true));
+        if (!policy::SnappyCompress(in, &c) || !policy::SnappyDecompress(c, &back) ||
+            !back.equals(in.to_string()))
+          bad++;
+      }
+    });
+  for (auto& x : th) x.join();
+  codec.SetParkHooks(flare::gpu::ParkHooks{});
+  ASSERT_EQ(bad.load(), 0);
+  printf("  latches: %d created, %d waits, %d signals, %d destroyed\n", g_park[0].load(), g_park[1].load(),
+         g_park[2].load(), g_park[3].load());
+  ASSERT_TRUE(g_park[0].load() > 0);
+  ASSERT_EQ(g_park[0].load(), g_park[1].load());
+  ASSERT_EQ(g_park[0].load(), g_park[2].load());
+  ASSERT_EQ(g_park[0].load(), g_park[3].load());
+}
+
+TEST_GPU(device_mask_init_and_shutdown) {
+  auto& codec = flare::gpu::SnappyGpuCodec::Instance();
+  ASSERT_EQ(codec.InitDevices(1), 1);
+  codec.Shutdown();
+  ASSERT_FALSE(codec.available());
+  const auto s0 = codec.stats();
+  cord_buf in, c, back;
+  in.append(pattern(70000, true));
+  ASSERT_TRUE(policy::SnappyCompress(in, &c));  // host codec while shut down
+  ASSERT_TRUE(policy::SnappyDecompress(c, &back));
+  const auto s1 = codec.stats();
+  ASSERT_EQ(s1.messages, s0.messages);
+  ASSERT_EQ(s1.cpu_messages - s0.cpu_messages, 2u);
+  ASSERT_TRUE(codec.InitDevices(0) >= 1);
+  cord_buf c2;
+  ASSERT_TRUE(policy::SnappyCompress(in, &c2));
+  ASSERT_EQ(codec.stats().messages - s1.messages, 1u);
+  ASSERT_EQ(c2.to_string(), c.to_string());
+  ASSERT_TRUE(back.equals(in.to_string()));
+}
+
+TEST_GPU(validate_only_on_device) {
+  auto& codec = flare::gpu::SnappyGpuCodec::Instance();
+  const std::string c = flat_compress(pattern(100000, true));
+  const auto s0 = codec.stats();
+  ASSERT_TRUE(flare::snappy::IsValidCompressedBuffer(c.data(), c.size()));
+  ASSERT_FALSE(flare::snappy::IsValidCompressedBuffer(c.data(), c.size() - 1));
+  ASSERT_EQ(codec.stats().messages - s0.messages, 2u);
+}
+
 int main(int argc, char** argv) {
   bool want_cpu = true, want_gpu = false;
   for (int i = 1; i < argc; ++i) {
@@ -384,6 +598,7 @@ int main(int argc, char** argv) {
   }
   if (want_gpu) {
     GlobalInitializeSnappyGpu();
+    flare::gpu::SnappyGpuCodec::Instance().SetMinGpuBytes(0);  // every body to the GPU
     if (!flare::gpu::SnappyGpuCodec::Instance().available()) {
       fprintf(stderr, "GPU codec unavailable: %s\n", flare::gpu::SnappyGpuCodec::Instance().error().c_str());
       return 2;

@@ -73,6 +73,8 @@ def main():
             verdict, out = ref.uncompress(comp, cap)
             for frag in (1, 3, 8160):
                 assert ref.uncompress(comp, cap, frag)[0] == verdict, name
+        # what UncompressAsMuchAsPossible (snappy.cc:1530-1535) leaves behind
+        pret, partial = ref.uncompress_as_much(comp, cap) if ok_src and verdict is not None else (0, b"")
         neg.append({
             "name": name,
             "hex": comp.hex(),
@@ -82,6 +84,9 @@ def main():
             "ok": verdict,
             "valid": ref.is_valid(comp),
             "output_fnv": "%016x" % fsg.fnv1a64(out) if verdict else None,
+            "partial_ret": pret,
+            "partial_len": len(partial),
+            "partial_fnv": "%016x" % fsg.fnv1a64(partial),
         })
     (HERE / "negative.json").write_text(json.dumps(neg, indent=1) + "\n")
 

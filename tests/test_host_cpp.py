@@ -34,5 +34,6 @@ def test_host_layer_gpu_cases(chunk_bytes):
         env["FLARE_SNAPPY_GPU_CHUNK_BYTES"] = chunk_bytes
     r = subprocess.run([str(_binary()), "--gpu"], capture_output=True, text=True, timeout=600, env=env)
     print(r.stdout)
+    print(r.stderr[-3000:])
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failures" in r.stdout
