@@ -119,20 +119,6 @@ __device__ __forceinline__ u32 dpp_incl_scan(u32 v) {
   return r;
 }
 
-// Inclusive max-scan over the 64 lanes, as dpp_incl_scan (0 is the identity:
-// lanes shifted in from outside a row read 0).
-__device__ __forceinline__ u32 dpp_incl_max(u32 v) {
-  u32 r = v;
-  r = max(r, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true));   // row_shr:1
-  r = max(r, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true));   // row_shr:2
-  r = max(r, (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xf, 0xf, true));   // row_shr:3
-  r = max(r, (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x114, 0xf, 0xe, false));  // row_shr:4, banks 1-3
-  r = max(r, (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x118, 0xf, 0xc, false));  // row_shr:8, banks 2-3
-  r = max(r, (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x142, 0xa, 0xf, false));  // row_bcast:15
-  r = max(r, (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x143, 0xc, 0xf, false));  // row_bcast:31
-  return r;
-}
-
 // ceil(len / step) for a pattern copy: len <= 64 and step >= 9 (pat_step of
 // offsets 1..15), so the answer is 1..8 -- counted instead of divided.
 __device__ __forceinline__ u32 pattern_pieces(u32 len, u32 step) {
@@ -628,13 +614,6 @@ __device__ __forceinline__ u32x4 lds_read16(const u8* p) {
   return v;
 }
 
-// Lane-ordered LDS store: when the lanes of ONE ds_write_* instruction write
-// overlapping (unaligned) ranges, every byte keeps the value of the highest
-// active lane covering it -- measured on gfx950 for b16/b32/b64/b128,
-// aligned and unaligned, under random lane masks
-// (tools/probes/lds_overlap_probe.hip, profiles/r2/lds_overlap_probe.txt).
-__device__ __forceinline__ void lds_write16(u8* p, u32x4 v) { __builtin_memcpy(p, &v, 16); }
-
 }  // namespace
 
 // One message, executed by the calling wave (see the pass-2 comment above).
@@ -866,23 +845,11 @@ __device__ __forceinline__ void exec_message(
       sbase = nsb;
     }
 
-    // piece -> tag lane: each tag writes its lane number at its first piece
-    // and an inclusive max-scan over the piece slots fills in the rest (lane
-    // numbers grow along the pieces); no per-piece store loop
-#if FSG_EXP_PMAP
-    if (lane < kMaxPieces / 4) reinterpret_cast<u32*>(pmap)[lane] = 0u;
-    wave_lds_fence();
-    if (fits) pmap[excl_pc] = (u8)lane;
-    wave_lds_fence();
-    const bool has = lane < tot_pc;
-    const u32 t = dpp_incl_max(pmap[lane]);
-#else
     if (fits)
       for (u32 p = 0; p < pc; ++p) pmap[excl_pc + p] = (u8)lane;
     wave_lds_fence();
     const bool has = lane < tot_pc;
     const u32 t = has ? pmap[lane] : 0u;
-#endif
     const u32 kind = is_lit ? 0u : (pat ? 2u : 1u);
     const u32 A = t_op;
     const u32 B = len | (excl_pc << 8) | (kind << 16) | ((pat ? coff : 0u) << 20);
@@ -909,24 +876,10 @@ __device__ __forceinline__ void exec_message(
       const int fe = (int)((op + obal) & ~15u) - (int)obal;
       if (fe > (int)flushed) flush_to((u32)fe);
     }
-    // Round A's pieces are stored 16 bytes each by one instruction: where
-    // their ranges overlap the highest lane (the later piece) wins, so each
-    // byte of a round-A piece ends up right (lds_write16); over-written tails
-    // that reach later near-copy pieces are overwritten when those are
-    // stored, exactly, in rounds B, before anything reads them.
-#if FSG_EXP_EXPAND
-    {
-      const u32x4 e = expand_pattern(xa, offT, sel_tab);
-      if (kT == 2) xa = e;
+    if (global_src) {
+      if (kT == 2) xa = expand_pattern(xa, offT, sel_tab);
+      store_exact(wdst, xa, n);
     }
-#else
-    if (global_src && kT == 2) xa = expand_pattern(xa, offT, sel_tab);
-#endif
-#if FSG_EXP_RA16
-    if (global_src) lds_write16(wdst, xa);
-#else
-    if (global_src) store_exact(wdst, xa, n);
-#endif
     wave_lds_fence();
 
     STAMP(4);
@@ -939,13 +892,8 @@ __device__ __forceinline__ void exec_message(
       const bool ready = !done && need_end <= wm;
       if (ready) {
         u32x4 x = lds_read16(sb + ((int)src - sbase));
-#if FSG_EXP_EXPAND
-        const u32x4 e = expand_pattern(x, offT, sel_tab);
-        store_exact(wdst, kT == 2 ? e : x, n);
-#else
         if (kT == 2) x = expand_pattern(x, offT, sel_tab);
         store_exact(wdst, x, n);
-#endif
       }
       wave_lds_fence();
       done = done || ready;
