@@ -10,7 +10,7 @@ CSRC     := $(PKG)/csrc/capi.hip $(PKG)/csrc/snappy_decode.hip $(PKG)/csrc/snapp
 CHDRS    := $(PKG)/csrc/snappy_device.h $(PKG)/csrc/snappy_lane_decode.h $(PKG)/csrc/snappy_pieces.h include/flare_snappy_gpu.h
 OBJDIR   := build/obj
 
-all: gpu host datagen oracle cpptests hostbench
+all: gpu host datagen oracle cpptests hostbench echobench
 
 gpu: $(LIB)/libflare_snappy_gpu.so
 
@@ -50,6 +50,14 @@ build/test_rpc_snappy_compress: tests/cpp/test_rpc_snappy_compress.cc $(HOST_HDR
 	  -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,$(abspath $(LIB)) -Wl,-rpath,'$$ORIGIN/../$(LIB)' \
 	  -Wl,-rpath,/opt/rocm/lib -pthread
 
+# Config 1: echo over loopback (baidu_std framing, SNAPPY request/response)
+echobench: build/echo_bench
+build/echo_bench: tools/echo_bench.cc $(HOST_HDRS) $(LIB)/libflare_rpc_snappy.so $(LIB)/libflare_datagen.so
+	@mkdir -p build
+	$(HOSTCXX) -o $@ $< -I$(PKG)/host -L$(LIB) -lflare_rpc_snappy -lflare_snappy_gpu -lflare_datagen \
+	  -L/opt/rocm/lib -lamdhip64 -ldl -Wl,-rpath,$(abspath $(LIB)) -Wl,-rpath,'$$ORIGIN/../$(LIB)' \
+	  -Wl,-rpath,/opt/rocm/lib -pthread
+
 # End-to-end rate of the host drop-in path (cord_buf in, cord_buf out)
 hostbench: build/host_bench
 build/host_bench: tools/host_bench.cc $(HOST_HDRS) $(LIB)/libflare_rpc_snappy.so $(LIB)/libflare_datagen.so
@@ -71,7 +79,7 @@ clean:
 	rm -rf build $(LIB)/*.so
 	$(MAKE) -C oracle clean
 
-.PHONY: all gpu host cpptests hostbench datagen oracle clean
+.PHONY: all gpu host cpptests hostbench echobench datagen oracle clean
 
 # Diagnostic build: exec_kernel phase stamps (s_memtime), never loaded by the
 # product path.  python tools/stamps.py runs it.

@@ -8,7 +8,8 @@ Default workload (the north-star target config): decompress
 65,536 x 64 KiB Zipf-text bodies; the same run also times C3 compress of the
 same bodies (the `encode` object).  Other workloads: c2-decompress (65,536 x
 4 KiB random), c3-compress, cm-decompress (power-law 256 B..1 MiB, strong
-scaling by default), c5-compress.
+scaling by default), c5-compress, and c1-echo (config 1: example/echo
+over loopback, QPS and latency; tools/echo_bench.cc).
 
 Multi-GPU: one process per GPU.  `--gpus N` without a
 WORLD_SIZE in the environment makes this process a launcher: it spawns N
@@ -75,7 +76,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c3-decompress", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c3-decompress", choices=sorted(WORKLOADS) + ["c1-echo"])
     ap.add_argument("--n-msgs", type=int, default=0, help="override messages per GPU (weak) / total (strong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -720,8 +721,56 @@ def cpu_baseline(op, batch, d_comp, c_off, comp_len, threads, with_single=True):
     return res
 
 
+def echo_main(args):
+    """BASELINE config 1: example/echo over loopback with
+    CompressType=snappy, 4 KiB request body, one client thread
+    (tools/echo_bench.cc).  `value` = QPS through the drop-in handler (its
+    host codec serves 4 KiB bodies: below the runtime's GPU threshold); the
+    same harness also runs every body through the GPU ("gpu"), without
+    compression ("none", the transport floor), and with the reference's own
+    Snappy (cpu_baseline, oracle/_ref loaded by the harness only here)."""
+    exe = REPO / "build" / "echo_bench"
+    if not exe.exists():
+        subprocess.run(["make", "-C", str(REPO), "echobench"], check=True, capture_output=True)
+    calls = max(1000, args.steps * 1000)
+
+    def run(codec, n):
+        r = subprocess.run([str(exe), "--codec", codec, "--calls", str(n), "--warmup", str(max(100, n // 20))],
+                           capture_output=True, text=True, timeout=600, cwd=str(REPO))
+        if r.returncode != 0:
+            raise RuntimeError(f"echo_bench --codec {codec}: rc {r.returncode}: {r.stdout} {r.stderr[-2000:]}")
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    main_run = run("runtime", calls)
+    modes = {"gpu": run("gpu", max(1000, calls // 4)), "none": run("none", calls)}
+    base = None
+    if not args.no_cpu_baseline:
+        ref = run("reference", calls)
+        base = {"value": ref["qps"], "unit": "QPS", "cores": 1, "kind": "reference",
+                "sample": f"{ref['calls']} echo calls through the reference's snappy.cc (oracle/_ref) on this "
+                          f"host, same harness; p50 {ref['p50_us']} us, p99 {ref['p99_us']} us, codec share "
+                          f"{ref['codec_share']}", "p50_us": ref["p50_us"], "p99_us": ref["p99_us"],
+                "codec_share": ref["codec_share"], "host": {"cpu_model": _cpu_model(), "nproc": os.cpu_count()}}
+    line = {
+        "metric": "QPS example/echo over loopback, CompressType=snappy, 4 KiB request body, 1 client thread",
+        "value": main_run["qps"], "unit": "QPS", "n_gpus": 1, "steps": main_run["calls"], "warmup": 0,
+        "ms_per_step": round(1e3 / main_run["qps"], 4), "higher_is_better": True, "scaling": "none",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (SURVEY.md §8(d) text generator, body 0, 4,093 B)",
+        "config": {"workload": "C1 echo: baidu_std loopback, SNAPPY request and response, 4,096-byte body",
+                   "codec": "drop-in handler (host codec below the GPU threshold)"},
+        "p50_us": main_run["p50_us"], "p99_us": main_run["p99_us"], "codec_share": main_run["codec_share"],
+        "modes": modes, "cpu_baseline": base,
+        "correct": {"errors": main_run["errors"] + sum(m["errors"] for m in modes.values()),
+                    "server_ok": main_run["server_ok"]},
+    }
+    print(json.dumps(line))
+
+
 def main(argv=None):
     args = parse(argv)
+    if args.workload == "c1-echo":
+        echo_main(args)
+        return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # launcher: spawn the ranks before this process touches the GPU
         sys.exit(launch(args.gpus, sys.argv[1:] if argv is None else list(argv)))

@@ -141,8 +141,8 @@ bool cpu_run(Kind kind, const cord_buf& in, cord_buf* out) {
   uint32_t ulen = 0;
   const size_t h = snappy::cpu::ReadHeader(p, n, &ulen, /*strict=*/false);
   if (h == 0 || !plausible_length(ulen, n)) return false;
-  tout.resize((size_t)ulen + 1);
-  if (!snappy::cpu::Decode(p, n, h, tout.data(), ulen)) return false;
+  tout.resize((size_t)ulen + 32);
+  if (!snappy::cpu::Decode(p, n, h, tout.data(), ulen, nullptr, tout.size())) return false;
   out->append(tout.data(), ulen);
   return true;
 }

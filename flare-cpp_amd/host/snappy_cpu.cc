@@ -39,8 +39,16 @@ inline size_t match_length(const uint8_t* s1, const uint8_t* s2, const uint8_t* 
 }
 
 // snappy.cc:156-196 (length n = len - 1 in 1..4 trailing bytes above 59).
-inline uint8_t* emit_literal(uint8_t* op, const uint8_t* lit, size_t len) {
+// Literals of <= 16 bytes copy 16 (the reference's fast path, :172-180): the
+// input has >= 15 bytes after any literal the main loop emits, and the output
+// buffer's MaxCompressedLength slack covers the over-write.
+inline uint8_t* emit_literal(uint8_t* op, const uint8_t* lit, size_t len, bool fast) {
   uint32_t n = (uint32_t)(len - 1);
+  if (fast && len <= 16) {
+    *op++ = (uint8_t)(n << 2);
+    memcpy(op, lit, 16);
+    return op + len;
+  }
   if (n < 60) {
     *op++ = (uint8_t)(n << 2);
   } else {
@@ -109,7 +117,7 @@ uint8_t* compress_fragment(const uint8_t* in, size_t n, uint8_t* op, uint16_t* t
         cand = base + table[h];
         table[h] = (uint16_t)(ip - base);
       } while (load32(ip) != load32(cand));
-      op = emit_literal(op, next_emit, (size_t)(ip - next_emit));
+      op = emit_literal(op, next_emit, (size_t)(ip - next_emit), true);
       // copies while the position after each one matches again (:404-444)
       uint32_t cand_bytes;
       uint64_t eight;
@@ -132,7 +140,7 @@ uint8_t* compress_fragment(const uint8_t* in, size_t n, uint8_t* op, uint16_t* t
     }
   }
 emit_remainder:
-  if (next_emit < ip_end) op = emit_literal(op, next_emit, (size_t)(ip_end - next_emit));
+  if (next_emit < ip_end) op = emit_literal(op, next_emit, (size_t)(ip_end - next_emit), false);
   return op;
 }
 
@@ -149,8 +157,33 @@ inline uint32_t load_le(const uint8_t* p, size_t k) {
   return v;
 }
 
+// Copy of len bytes from op - off to op; `room` = writable bytes from op
+// (>= len).  With >= len + 16 of room it over-copies in 8-byte steps like
+// IncrementalCopyFastPath (snappy.cc:140-152): an offset below 8 first
+// widens the pattern to 8 bytes.
+inline void copy_back(uint8_t* d, size_t off, size_t len, size_t room) {
+  const uint8_t* s = d - off;
+  if (room >= len + 16) {
+    if (off >= 8) {
+      for (size_t i = 0; i < len; i += 8) memcpy(d + i, s + i, 8);
+      return;
+    }
+    if (off >= len) {
+      memcpy(d, s, 8);
+      if (len > 8) memcpy(d + 8, s + 8, 8);
+      return;
+    }
+  }
+  if (off >= len) {
+    memcpy(d, s, len);
+  } else {
+    for (size_t i = 0; i < len; ++i) d[i] = s[i];  // IncrementalCopy :98-103
+  }
+}
+
 template <bool kWrite>
-bool decode_tags(const uint8_t* ip, const uint8_t* end, uint8_t* out, uint32_t expected, size_t* produced) {
+bool decode_tags(const uint8_t* ip, const uint8_t* end, uint8_t* out, uint32_t expected, size_t out_cap,
+                 size_t* produced) {
   size_t op = 0;
   bool ok = false;
   for (;;) {
@@ -167,6 +200,12 @@ bool decode_tags(const uint8_t* ip, const uint8_t* end, uint8_t* out, uint32_t e
       if (len32 >= 61) len32 = load_le(ip, extra) + 1u;  // uint32: 0xffffffff + 1 == 0
       ip += extra;
       const size_t len = len32;
+      if (kWrite && len <= 16 && (size_t)(end - ip) >= 16 && op + 16 <= out_cap && len <= expected - op) {
+        memcpy(out + op, ip, 16);  // TryFastAppend (:1386-1398)
+        op += len;
+        ip += len;
+        continue;
+      }
       // the writer takes what the input holds and the header allows (:744-761,
       // SlowAppend :1424-1451); any shortfall fails the stream
       const size_t take = std::min({len, (size_t)(end - ip), (size_t)expected - op});
@@ -187,15 +226,7 @@ bool decode_tags(const uint8_t* ip, const uint8_t* end, uint8_t* out, uint32_t e
       // offset 0 or beyond the output so far; no room left (:1200-1210,
       // :1410-1413, :1463-1466): all-or-nothing
       if (off - 1u >= op || (size_t)expected - op < len) break;
-      if (kWrite) {
-        uint8_t* d = out + op;
-        const uint8_t* s = d - off;
-        if (off >= len) {
-          memcpy(d, s, len);
-        } else {
-          for (size_t i = 0; i < len; ++i) d[i] = s[i];  // IncrementalCopy :98-103
-        }
-      }
+      if (kWrite) copy_back(out + op, off, len, out_cap - op);
       op += len;
     }
   }
@@ -370,21 +401,22 @@ size_t Compress(const uint8_t* in, size_t n, uint8_t* out) {
   return (size_t)(op - out);
 }
 
-bool Decode(const uint8_t* in, size_t n, size_t hdr, uint8_t* out, uint32_t expected, size_t* produced) {
-  return decode_tags<true>(in + hdr, in + n, out, expected, produced);
+bool Decode(const uint8_t* in, size_t n, size_t hdr, uint8_t* out, uint32_t expected, size_t* produced,
+            size_t out_cap) {
+  return decode_tags<true>(in + hdr, in + n, out, expected, out_cap > expected ? out_cap : expected, produced);
 }
 
 bool Uncompress(const uint8_t* in, size_t n, uint8_t* out, size_t out_cap, bool strict) {
   uint32_t ulen = 0;
   const size_t h = ReadHeader(in, n, &ulen, strict);
   if (h == 0 || ulen > out_cap) return false;
-  return decode_tags<true>(in + h, in + n, out, ulen, nullptr);
+  return decode_tags<true>(in + h, in + n, out, ulen, out_cap, nullptr);
 }
 
 bool IsValid(const uint8_t* in, size_t n) {
   uint32_t ulen = 0;
   const size_t h = ReadHeader(in, n, &ulen, false);
-  return h != 0 && decode_tags<false>(in + h, in + n, nullptr, ulen, nullptr);
+  return h != 0 && decode_tags<false>(in + h, in + n, nullptr, ulen, 0, nullptr);
 }
 
 }  // namespace flare::snappy::cpu

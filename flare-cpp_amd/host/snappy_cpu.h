@@ -42,9 +42,11 @@ size_t Compress(const uint8_t* in, size_t n, uint8_t* out);
 // Returns true iff the reference accepts the stream.  *produced (optional)
 // receives the bytes the reference's scattered writer holds when it stops:
 // every completed tag, plus the part of a literal that fit the input and the
-// header length (copies are all-or-nothing).  `out` needs `expected` bytes.
+// header length (copies are all-or-nothing).  `out` needs `expected` bytes;
+// `out_cap` > expected lets the fast paths over-write up to 16 bytes past
+// the produced bytes (never past out_cap).
 bool Decode(const uint8_t* in, size_t n, size_t hdr, uint8_t* out, uint32_t expected,
-            size_t* produced = nullptr);
+            size_t* produced = nullptr, size_t out_cap = 0);
 
 // Header (lenient unless `strict`) + Decode.  `out` needs the header length.
 bool Uncompress(const uint8_t* in, size_t n, uint8_t* out, size_t out_cap, bool strict);

@@ -37,3 +37,33 @@ def test_host_layer_gpu_cases(chunk_bytes):
     print(r.stderr[-3000:])
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 failures" in r.stdout
+
+
+ECHO = REPO / "build" / "echo_bench"
+
+
+@pytest.mark.parametrize("codec", ["runtime", "none"])
+def test_echo_loopback_cpu(codec):
+    """Config 1's harness (tools/echo_bench.cc): baidu_std echo over loopback,
+    SNAPPY request and response, a 4,096-byte body; every echo comes back intact."""
+    if not ECHO.exists():
+        subprocess.run(["make", "-C", str(REPO), "echobench"], check=True, capture_output=True)
+    r = subprocess.run([str(ECHO), "--codec", codec, "--calls", "300", "--warmup", "20"], capture_output=True,
+                       text=True, timeout=120, cwd=str(REPO))
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["errors"] == 0 and d["server_ok"] and d["body_bytes"] == 4096 and d["qps"] > 0
+
+
+@pytest.mark.gpu
+def test_echo_loopback_gpu():
+    """The same echo with every body sent through the GPU (threshold 0)."""
+    if not ECHO.exists():
+        subprocess.run(["make", "-C", str(REPO), "echobench"], check=True, capture_output=True)
+    r = subprocess.run([str(ECHO), "--codec", "gpu", "--calls", "300", "--warmup", "20"], capture_output=True,
+                       text=True, timeout=120, cwd=str(REPO))
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["errors"] == 0 and d["server_ok"] and d["gpu_messages"] == 4 * 320
