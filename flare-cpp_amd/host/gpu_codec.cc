@@ -129,7 +129,7 @@ const uint8_t* flatten(const cord_buf& in, std::vector<uint8_t>* tmp) {
 inline bool plausible_length(uint32_t ulen, size_t in_len) { return (uint64_t)ulen <= 22ull * in_len + 64; }
 
 bool cpu_run(Kind kind, const cord_buf& in, cord_buf* out) {
-  thread_local std::vector<uint8_t> tin, tout;
+  std::vector<uint8_t> tin, tout;  // per call: no thread_local (see snappy_cpu.cc)
   const uint8_t* p = flatten(in, &tin);
   const size_t n = in.size();
   if (kind == kCompress) {

@@ -43,15 +43,17 @@ int add_range(void* p, size_t n, OutSlab* slab) {
   return i;
 }
 
+std::atomic<int> g_last_hit{-1};  // a hint (no thread_local: see snappy_cpu.cc)
+
 const Range* find_range(const void* p, size_t n) {
-  static thread_local int last = -1;
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
   const int cnt = g_nranges.load(std::memory_order_acquire);
   auto hit = [&](int i) { return a >= g_ranges[i].base && a + n <= g_ranges[i].base + g_ranges[i].size; };
+  const int last = g_last_hit.load(std::memory_order_relaxed);
   if (last >= 0 && last < cnt && hit(last)) return &g_ranges[last];
   for (int i = cnt - 1; i >= 0; --i)
     if (hit(i)) {
-      last = i;
+      g_last_hit.store(i, std::memory_order_relaxed);
       return &g_ranges[i];
     }
   return nullptr;

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 
 namespace flare::snappy::cpu {
 
@@ -390,7 +391,16 @@ size_t Compress(const uint8_t* in, size_t n, uint8_t* out) {
     v >>= 7;
   }
   *op++ = (uint8_t)v;
-  static thread_local uint16_t table[kMaxTable];
+  // the hash table per call, as WorkingMemory (snappy.cc:247-271): on the
+  // stack up to 4096 entries, else on the heap (no thread_local: TLS access
+  // from this library measured 2x slower once the HIP runtime is up)
+  uint16_t small[4096];
+  std::unique_ptr<uint16_t[]> big;
+  uint16_t* table = small;
+  if (n > 4096) {
+    big.reset(new uint16_t[kMaxTable]);
+    table = big.get();
+  }
   for (size_t pos = 0; pos < n; pos += kFragment) {
     const size_t frag = std::min(kFragment, n - pos);
     uint32_t entries = 256;  // WorkingMemory::GetHashTable (:247-271)

@@ -18,11 +18,13 @@
 //   echo_bench --codec reference    the reference's own Snappy (oracle/_ref,
 //                                   loaded only here, for bench.py's
 //                                   cpu_baseline leg)
+//   echo_bench --codec host         the runtime's host codec called directly
 //   echo_bench --codec none         COMPRESS_TYPE_NONE: the transport floor
 // Prints one JSON object: calls, QPS, p50/p99/mean latency (us) and the share
 // of client+server time spent inside the compress handlers.
 #include <arpa/inet.h>
 #include <dlfcn.h>
+#include <sched.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
@@ -37,6 +39,8 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <hip/hip_runtime.h>
 
 #include "baidu_rpc_protocol.h"
 #include "compress.h"
@@ -208,12 +212,21 @@ int main(int argc, char** argv) {
   std::string codec = "runtime";
   int calls = 20000, warmup = 500;
   size_t msg_len = 4093;
-  for (int i = 1; i + 1 < argc; i += 2) {
+  for (int i = 1; i + 1 < argc; ++i) {
     if (!strcmp(argv[i], "--codec")) codec = argv[i + 1];
     if (!strcmp(argv[i], "--calls")) calls = atoi(argv[i + 1]);
     if (!strcmp(argv[i], "--warmup")) warmup = atoi(argv[i + 1]);
     if (!strcmp(argv[i], "--message-bytes")) msg_len = (size_t)atol(argv[i + 1]);
   }
+  for (int i = 1; i < argc; ++i)
+    if (!strcmp(argv[i], "--init-hip")) {  // diagnostic: HIP runtime up, unused
+      cpu_set_t a0, a1;
+      sched_getaffinity(0, sizeof(a0), &a0);
+      int n = 0;
+      (void)hipGetDeviceCount(&n);
+      sched_getaffinity(0, sizeof(a1), &a1);
+      fprintf(stderr, "affinity cpus before %d after %d\n", CPU_COUNT(&a0), CPU_COUNT(&a1));
+    }
   CompressType type = COMPRESS_TYPE_SNAPPY;
   if (codec == "runtime" || codec == "gpu") {
     GlobalInitializeSnappyGpu();  // the drop-in: global.cc:372-376's registration
@@ -223,6 +236,16 @@ int main(int argc, char** argv) {
     g_comp = h->Compress;
     g_decomp = h->Decompress;
     ResetCompressHandlersForTesting();
+  } else if (codec == "host") {
+    // the runtime's host codec called directly (no runtime dispatch)
+    g_comp = [](const Message& m, cord_buf* b) {
+      cord_buf pb;
+      return m.SerializeToCordBuf(&pb) && flare::gpu::CpuCompress(pb, b);
+    };
+    g_decomp = [](const cord_buf& d, Message* m) {
+      cord_buf pb;
+      return flare::gpu::CpuUncompress(d, &pb) && m->ParseFromCordBuf(pb);
+    };
   } else if (codec == "reference") {
     const char* path = getenv("FLARE_SNAPPY_REF_LIB");
     void* L = dlopen(path ? path : "oracle/_ref/libsnappy_ref.so", RTLD_NOW);
