@@ -101,7 +101,7 @@ size_t g_out_total = 0;
 size_t out_cap_bytes() {
   static const size_t cap = [] {
     const char* e = getenv("FLARE_SNAPPY_GPU_PINNED_OUT_BYTES");
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)(4ull << 30);
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)(16ull << 30);
   }();
   return cap;
 }

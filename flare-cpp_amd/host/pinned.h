@@ -12,7 +12,7 @@ namespace flare::gpu {
 // released it.
 struct OutSlab;
 // nullptr when the pool is at its cap (FLARE_SNAPPY_GPU_PINNED_OUT_BYTES,
-// default 4 GiB) or pinned memory is unavailable: the caller copies instead.
+// default 16 GiB) or pinned memory is unavailable: the caller copies instead.
 OutSlab* AcquireOutSlab(size_t bytes);  // holds one reference
 uint8_t* OutSlabData(OutSlab* s);
 void OutSlabRef(OutSlab* s);

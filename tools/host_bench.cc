@@ -4,7 +4,11 @@
 // SnappyGpuCodec::CompressBatch / UncompressBatch (gather into pinned staging,
 // H2D, kernels, D2H, append to the output cord_bufs -- the socket -> cord_buf
 // -> socket path of BASELINE.json north_star, minus the socket).
-//   ./build/host_bench [messages] [size] [reps]      (defaults 16384 65536 3)
+//   ./build/host_bench [messages] [size] [reps] [pinned]   (defaults 16384 65536 3 0)
+// pinned = 1 installs the pinned block allocator first (fsh_use_pinned_blocks):
+// input blocks are then read by the GPU directly and no staging copy is made;
+// outputs are adopted from pinned slabs either way (so the compressed
+// cord_bufs feed the decompress leg without staging too).
 // Prints one JSON line.  Byte-checks every round trip.
 #include <chrono>
 #include <cstdio>
@@ -23,6 +27,11 @@ int main(int argc, char** argv) {
   const size_t n = argc > 1 ? strtoull(argv[1], nullptr, 10) : 16384;
   const size_t size = argc > 2 ? strtoull(argv[2], nullptr, 10) : 65536;
   const int reps = argc > 3 ? atoi(argv[3]) : 3;
+  const bool pinned = argc > 4 && atoi(argv[4]) != 0;
+  if (pinned && flare::gpu::UsePinnedBlocks() != 0) {
+    fprintf(stderr, "pinned blocks unavailable\n");
+    return 1;
+  }
   auto& codec = flare::gpu::SnappyGpuCodec::Instance();
   if (!codec.available()) {
     fprintf(stderr, "GPU codec unavailable: %s\n", codec.error().c_str());
@@ -67,11 +76,15 @@ int main(int argc, char** argv) {
     best_d = std::min(best_d, std::chrono::duration<double>(t2 - t1).count());
   }
   const double gib = 1024.0 * 1024.0 * 1024.0;
+  const auto st = codec.stats();
   printf("{\"messages\": %zu, \"size\": %zu, \"ratio\": %.3f, \"compress_gib_s\": %.3f, "
          "\"decompress_gib_s\": %.3f, \"compress_ms\": %.2f, \"decompress_ms\": %.2f, \"round_trip_ok\": %s, "
-         "\"path\": \"cord_buf (8160-B blocks) -> pinned gather -> H2D -> kernels -> D2H -> cord_buf append, "
-         "chunked over 3 streams\"}\n",
+         "\"pinned_blocks\": %s, \"adopted\": %llu, \"device_messages\": %llu, "
+         "\"path\": \"cord_buf (8160-B blocks) -> %s -> kernels -> D2H into pinned slabs -> adopted "
+         "(append_user_data), chunked over 3 streams\"}\n",
          n, size, raw_bytes / comp_bytes, raw_bytes / best_c / gib, raw_bytes / best_d / gib, best_c * 1e3,
-         best_d * 1e3, ok_all ? "true" : "false");
+         best_d * 1e3, ok_all ? "true" : "false", pinned ? "true" : "false", (unsigned long long)st.adopted,
+         (unsigned long long)st.messages,
+         pinned ? "GPU gather from pinned blocks" : "memcpy into pinned staging + H2D");
   return ok_all ? 0 : 2;
 }
