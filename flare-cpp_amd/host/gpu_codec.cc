@@ -626,10 +626,14 @@ struct SnappyGpuCodec::Impl {
   }
 
   bool process(const cord_buf& in, cord_buf* out, Kind kind) {
-    ensure_started();
-    if (n_devs.load(std::memory_order_relaxed) > 0 && in.size() >= min_bytes.load(std::memory_order_relaxed)) {
-      Request r{&in, out, kind};
-      if (submit(&r)) return r.ok;
+    // devices start on the first body that needs one: a process whose bodies
+    // all stay below the threshold never initialises HIP
+    if (in.size() >= min_bytes.load(std::memory_order_relaxed)) {
+      ensure_started();
+      if (n_devs.load(std::memory_order_relaxed) > 0) {
+        Request r{&in, out, kind};
+        if (submit(&r)) return r.ok;
+      }
     }
     ctr.cpu_messages += 1;
     return cpu_run(kind, in, out);
