@@ -144,6 +144,32 @@ __global__ __launch_bounds__(64) void index_kernel(
   __shared__ u32 ring[(kRingDwords + 5) * kWave];
 
   const u32 lane = threadIdx.x;
+  // Tag table (the role of char_table, snappy.cc:516-549): per tag byte c,
+  // bits 0-2 extra bytes, 3 long literal, 4 literal, 8-15 advance without a
+  // long literal's length, 16-23 length (short literal / copies), 24-26 a
+  // COPY_1's offset bits 8-10.
+  __shared__ u32 tagtab[256];
+#pragma unroll
+  for (u32 q = 0; q < 4; ++q) {
+    const u32 c = lane * 4 + q, type = c & 3, l0 = (c >> 2) + 1;
+    u32 nb, len, lit = 0, ll = 0, hi3 = 0;
+    if (type == 0) {
+      lit = 1;
+      nb = l0 > 60 ? l0 - 60 : 0;
+      ll = nb ? 1 : 0;
+      len = nb ? 0 : l0;
+    } else if (type == 1) {
+      nb = 1;
+      len = 4 + ((c >> 2) & 7);
+      hi3 = c >> 5;
+    } else {
+      nb = type == 2 ? 2 : 4;
+      len = l0;
+    }
+    const u32 adv = 1 + nb + (lit && !ll ? len : 0);
+    tagtab[c] = nb | (ll << 3) | (lit << 4) | (adv << 8) | (len << 16) | (hi3 << 24);
+  }
+  __syncthreads();
   const bool strict = flags & 2u;
   const bool validate = flags & 1u;
   const u32 m = blockIdx.x * blockDim.x + lane;
@@ -295,29 +321,26 @@ __global__ __launch_bounds__(64) void index_kernel(
       const u32 bsh = (ip + ibal) & 3;
       const u32 t0 = alignbyte(hi, lo, bsh);          // bytes ip..ip+3
       const u32 ext = alignbyte(hi >> (8 * bsh), t0, 1);  // bytes ip+1..ip+4
-      // branch-free tag decode (DecompressAllTags :716-787, char_table :516-549):
-      // the 0..4 bytes after the tag byte are a literal's length or a copy's
-      // offset, masked to their count nb.  Written as selects and masks so
-      // the compiler keeps it free of exec-mask branches.
+      // tag decode through the tag table (DecompressAllTags :716-787): the
+      // 0..4 bytes after the tag byte are a literal's length or a copy's
+      // offset, masked to their count nb; selects, no exec-mask branches.
       const u32 c = t0 & 0xffu;
-      const u32 type = c & 3;
-      const u32 l0 = (c >> 2) + 1;
-      const u32 litm = type == 0 ? ~0u : 0u;
-      const u32 nbl = (l0 > 60 ? l0 - 60 : 0u) & litm;        // 1..4 length bytes (:744-750)
-      const u32 nb = ((0x4210u >> (type << 2)) & 0xfu) | nbl;  // copies: 1, 2, 4
+      const u32 e = tagtab[c];
+      const u32 nb = e & 7u;
       const u32 val = ext & (0xffffffffu >> ((32 - 8 * nb) & 31));
-      const u32 lc = type == 1 ? 4 + ((c >> 2) & 7) : l0;
-      const u32 len = nbl ? val + 1u : lc;  // uint32 wrap: 0xffffffff+1 == 0
+      const bool longlit = (e & 8u) != 0;
+      const u32 len = longlit ? val + 1u : (e >> 16) & 0xffu;  // uint32 wrap: 0xffffffff+1 == 0
+      const u32 type = (e & 16u) ? 0u : 1u;  // 0 = literal (only literal-ness is used below)
       // The walk advances over every tag below lim whether or not it passed
       // its checks, so the checks stay off the ip -> ip dependency chain.
       // After the first failing tag the status is final (kCorrupt): what the
       // walk reads from there on only sets bits in the LDS ring, which are
       // never stored for a corrupt message, and ring indices are masked.
       const bool look = ip < lim;
-      const u32 nx = ip + 1 + nb + (len & litm);
+      const u32 nx = ip + ((e >> 8) & 0xffu) + (longlit ? len : 0u);
       const u32 ip_next = look ? nx : ip;
       if (j + 1 < kIdxTags) ring_read(ip_next, lo, hi);
-      const u32 coff = val | ((type == 1 ? c >> 5 : 0u) << 8);
+      const u32 coff = val | ((e >> 16) & 0x700u);
       // tag bytes and literal bytes present (:744-761), compared against the
       // bytes left after the tag so no sum can wrap (a 4-byte literal length
       // of 0xfffffffa..0xfffffffe would wrap nx back onto its own length
