@@ -56,8 +56,11 @@ constexpr u32 kBigStageBytes = 16 * kBigStageChunks;
 
 // ---- pass 2 geometry
 constexpr u32 kWavesPerBlock = 4;
-constexpr u32 kTagRing = 512;                // tag positions per wave (LDS)
-constexpr u32 kFillWords = 16;               // bitmap words per fill (512 input bytes)
+#ifndef FSG_TAG_RING
+#define FSG_TAG_RING 512
+#endif
+constexpr u32 kTagRing = FSG_TAG_RING;       // tag positions per wave (LDS)
+constexpr u32 kFillWords = kTagRing / 32;    // bitmap words per fill (<= kTagRing / 2 tags)
 constexpr u32 kMaxPieces = 64;
 // bm_base[m] with this bit set: the message is one literal starting at the
 // low bits (set by pass 1; bitmap bases stay below 2^31 words)
@@ -620,7 +623,8 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
 //             window, already stored) load from global memory -- one round
 //             trip, all independent -- and land in the window;
 //   rounds B  near copies (source inside the window) resolve in LDS in
-//             dependency rounds;
+//             dependency rounds, OR-ing their bytes into the zeroed window
+//             ahead of the write front (five aligned ds_or_b32 per piece);
 //   flush     completed 16-byte blocks go to global memory, 1 KiB per wave
 //             instruction.
 // The window slides (keeping >= 2 KiB of history) when a group would overrun
@@ -628,13 +632,41 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
 // global-to-global, 1 KiB per instruction.
 // ===========================================================================
 namespace {
-constexpr u32 kWindow = 4096;  // LDS output window per wave
-constexpr u32 kKeep = 2048;    // history kept when the window slides
+#ifndef FSG_WINDOW
+#define FSG_WINDOW 4096
+#define FSG_KEEP 2048
+#endif
+constexpr u32 kWindow = FSG_WINDOW;  // LDS output window per wave
+constexpr u32 kKeep = FSG_KEEP;      // history kept when the window slides
 
 __device__ __forceinline__ u32x4 lds_read16(const u8* p) {
   u32x4 v;
   __builtin_memcpy(&v, p, 16);
   return v;
+}
+
+// OR n (1..16) bytes of v into the window at byte offset w, whose bytes
+// there are zero: five aligned ds_or_b32 whatever w and n, so the LDS time
+// is fixed per instruction instead of per misaligned lane, and no size
+// branches.  Bytes past n are masked to zero, so nothing lands past w + n.
+__device__ __forceinline__ void or_store(u8* sb, u32 w, u32x4 v, u32 n) {
+#pragma unroll
+  for (u32 k = 0; k < 4; ++k) {
+    const u32 have = n > 4 * k ? n - 4 * k : 0u;
+    v[k] &= have >= 4 ? 0xffffffffu : (have ? 0xffffffffu >> (32 - 8 * have) : 0u);
+  }
+  const u32 b = w & 3;
+  const u32 o0 = v[0] << (8 * b);
+  const u32 o1 = b ? alignbyte(v[1], v[0], 4 - b) : v[1];
+  const u32 o2 = b ? alignbyte(v[2], v[1], 4 - b) : v[2];
+  const u32 o3 = b ? alignbyte(v[3], v[2], 4 - b) : v[3];
+  const u32 o4 = b ? v[3] >> (32 - 8 * b) : 0u;
+  u32* d = reinterpret_cast<u32*>(sb) + (w >> 2);
+  __hip_atomic_fetch_or(d + 0, o0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_or(d + 1, o1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_or(d + 2, o2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_or(d + 3, o3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_or(d + 4, o4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 }  // namespace
@@ -688,6 +720,15 @@ __device__ __forceinline__ void exec_message(
   u32 head = 0, tail = 0, scan = ip0 >> 5, op = op0;
   int sbase = (int)((op0 + obal) & ~15u) - (int)obal;  // output position of sb[0]
   u32 flushed = op0;  // output [op0, flushed) is in global memory
+  // window bytes from the write front up to zero_end are zero, so rounds B
+  // can OR their pieces in (or_store)
+  auto zero_from = [&](u32 from) {  // 1 KiB of zeros at a 16-aligned offset
+    const u32 i = from + 16 * lane;
+    if (i < kWindow + 32) *reinterpret_cast<u32x4*>(sb + i) = u32x4{0, 0, 0, 0};
+  };
+  zero_from(0);
+  u32 zero_end = 1024;
+  wave_lds_fence();
   // next fill, prefetched: lane l holds word scan + l / 4 and takes its byte l % 4
   auto fill_word = [&](u32 sc) -> u32 {
     const u32 wi = sc + (lane >> 2);
@@ -794,6 +835,9 @@ __device__ __forceinline__ void exec_message(
       // >= 16 flushed bytes precede it (a copy reading before the window
       // then reads only stored bytes); its head comes from the literal's tail.
       sbase = (int)((op + obal) & ~15u) - (int)obal - 16;
+      zero_from(0);
+      zero_end = 1024;
+      wave_lds_fence();
       if (lane < 2) {
         const u32 lo = (u32)sbase + 16 * lane;
         if (lo < op) {
@@ -866,7 +910,13 @@ __device__ __forceinline__ void exec_message(
         wave_lds_fence();
       }
       sbase = nsb;
+      zero_end = (keep + 15) & ~15u;  // the copied blocks end in zeros past op
     }
+    while (op + tot_len + 20 - sbase > zero_end) {  // the group's OR stores land in zeros
+      zero_from(zero_end);
+      zero_end += 1024;
+    }
+    wave_lds_fence();
 
     if (fits)
       for (u32 p = 0; p < pc; ++p) pmap[excl_pc + p] = (u8)lane;
@@ -901,7 +951,7 @@ __device__ __forceinline__ void exec_message(
     }
     if (global_src) {
       if (kT == 2) xa = expand_pattern(xa, offT, sel_tab);
-      store_exact(wdst, xa, n);
+      store_exact(wdst, xa, n);  // (or_store here measured 4% slower)
     }
     wave_lds_fence();
 
@@ -916,7 +966,7 @@ __device__ __forceinline__ void exec_message(
       if (ready) {
         u32x4 x = lds_read16(sb + ((int)src - sbase));
         if (kT == 2) x = expand_pattern(x, offT, sel_tab);
-        store_exact(wdst, x, n);
+        or_store(sb, (u32)((int)dst - sbase), x, n);
       }
       wave_lds_fence();
       done = done || ready;
@@ -955,7 +1005,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
   // per wave: the tag ring, then the output window; a large message's index
   // walk stages its input over both (kBigStageBytes + 16 <= their size)
   __shared__ __attribute__((aligned(16))) u8 wl_s[kWavesPerBlock][4 * kTagRing + kWindow + 32];
-  __shared__ u8 pmap_s[kWavesPerBlock][kMaxPieces];
+  __shared__ __attribute__((aligned(16))) u8 pmap_s[kWavesPerBlock][kMaxPieces];
   __shared__ u32x4 sel_tab[16];
   static_assert(kBigStageBytes + 16 <= 4 * kTagRing + kWindow + 32, "stage fits the wave's LDS");
 
