@@ -632,6 +632,9 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
 // global-to-global, 1 KiB per instruction.
 // ===========================================================================
 namespace {
+#ifndef FSG_FAR_SC1
+#define FSG_FAR_SC1 1
+#endif
 #ifndef FSG_WINDOW
 #define FSG_WINDOW 4096
 #define FSG_KEEP 2048
@@ -671,6 +674,22 @@ __device__ __forceinline__ void or_store(u8* sb, u32 w, u32x4 v, u32 n) {
 
 }  // namespace
 
+// A far copy's 16 source bytes: output this wave stored in an earlier group,
+// read from the slot with an sc1 load, which is served by L2 and bypasses
+// this CU's L1 (MI355X_MICROARCH.md, visibility table).  Why that matters:
+// an L1 line can be filled while part of it is still unwritten -- a far load
+// just after a long literal's window restart, or the neighbouring message's
+// slot sharing a 128-byte line -- and the vector L1 is not specified to pick
+// up later stores.  Ordering in L2: a wave's vector memory operations return
+// in issue order, loads and stores alike, and every far source was flushed
+// at least one group before it is read, behind that group's waited tag loads
+// ("far copies").  src + 16 <= op <= the slot length
+// (far sources end >= 16 bytes below the window base, which is <= op - 16), so
+// the range check never clips a needed byte.
+__device__ __forceinline__ u32x4 far_load(__amdgpu_buffer_rsrc_t r, u32 off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+}
+
 // One message, executed by the calling wave (see the pass-2 comment above).
 __device__ __forceinline__ void exec_message(
     u32 m, const u8* __restrict__ in, const u64* __restrict__ in_off,
@@ -690,6 +709,11 @@ __device__ __forceinline__ void exec_message(
   if (st != kOk) return;
   const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
   const u32 obal = (u32)(reinterpret_cast<uintptr_t>(ob) & 15);
+#if FSG_FAR_SC1
+  // the message's slot as a buffer: far copies load through it past L1
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc(ob - obal, (short)0, (int)(expected + obal), 0x00020000);
+#endif
 
   if ((bmb & kSingleLiteral) && op1 == expected && op0 == 0) {
     // one literal (checked by pass 1): a straight copy, 4 KiB per step with
@@ -942,7 +966,11 @@ __device__ __forceinline__ void exec_message(
     const bool global_src = has && (kT == 0 || (int)src < sbase);
     u32x4 xa = u32x4{0, 0, 0, 0};
     if (global_src)
+#if FSG_FAR_SC1
+      xa = kT == 0 ? load16_clamped(ib, src, n_in, ibal) : far_load(orsrc, src + obal);
+#else
       xa = kT == 0 ? load16_clamped(ib, src, n_in, ibal) : load16_clamped(ob, src, expected, obal);
+#endif
     // the previous group's completed blocks are flushed while these loads are
     // in flight (far sources lie before the window: flushed long ago)
     {

@@ -413,3 +413,25 @@ def test_large_message_segments(gpu, oracle):
         ok, ulen, ref = oracle.uncompress(c, cap=1 << 21)
         assert ok, i
         assert s == fsg.FSG_OK and o[:ulen] == ref, (i, s)
+
+
+def test_far_copies_at_window_edge(gpu, oracle):
+    """Copies whose sources lie a few bytes either side of pass 2's window base
+    (tests/window_edge.py replays the kernel's group/window rules to place
+    them): far copies read back output stored to global memory in earlier
+    groups, including 16-byte loads straddling the base, right after window
+    slides and long-literal restarts.  Decoded bytes equal the construction's
+    and the oracle's, messages side by side in 16-byte-aligned slots."""
+    from window_edge import edge_stream
+    rng = np.random.default_rng(31)
+    comps, raws, n_edge = [], [], 0
+    for i in range(800):
+        c, raw, e = edge_stream(rng, int(rng.integers(2000, 40000)))
+        comps.append(c); raws.append(raw); n_edge += e
+    assert n_edge > 5000
+    outs, ol, st = gpu.decompress(comps, [len(r) for r in raws])
+    for i, (c, raw, o, s) in enumerate(zip(comps, raws, outs, st)):
+        assert s == fsg.FSG_OK and o == raw, i
+    for i in range(0, 800, 97):
+        ok, ulen, ref = oracle.uncompress(comps[i], cap=len(raws[i]))
+        assert ok and ref == raws[i], i

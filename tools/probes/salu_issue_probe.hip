@@ -17,7 +17,7 @@
 typedef uint32_t u32;
 typedef uint64_t u64;
 
-constexpr int kIters = 512;
+constexpr int kIters = 512;  // per launch of the memtime runs; event runs take a count
 
 enum Mode { SALU, VALU, MIX, MIX2 };
 static const char* kNames[] = {"salu", "valu", "salu+valu 1:1", "salu+valu 1:2"};
@@ -27,7 +27,7 @@ static const char* kNames[] = {"salu", "valu", "salu+valu 1:1", "salu+valu 1:2"}
                   " %3, %3, %8\n\t" op " %4, %4, %8\n\t" op " %5, %5, %8\n\t" op \
                   " %6, %6, %8\n\t" op " %7, %7, %8"                          \
                : "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3), "+s"(s4), "+s"(s5), "+s"(s6), "+s"(s7) \
-               : "s"(k))
+               : "s"(k) : "scc")
 #define V8(op)                                                         \
   asm volatile(op " %0, %0, %8\n\t" op " %1, %1, %8\n\t" op " %2, %2, %8\n\t" op \
                   " %3, %3, %8\n\t" op " %4, %4, %8\n\t" op " %5, %5, %8\n\t" op \
@@ -35,21 +35,27 @@ static const char* kNames[] = {"salu", "valu", "salu+valu 1:1", "salu+valu 1:2"}
                : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3), "+v"(v4), "+v"(v5), "+v"(v6), "+v"(v7) \
                : "v"(kv))
 
+__device__ __forceinline__ u64 memtime() {
+  u64 t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
 template <int MODE>
-__global__ __launch_bounds__(1024) void probe(u32 k, u64* cycles, u32* out) {
+__global__ __launch_bounds__(1024) void probe(u32 k, u64* cycles, u32* out, int iters) {
   u32 s0 = k, s1 = k + 1, s2 = k + 2, s3 = k + 3, s4 = k + 4, s5 = k + 5, s6 = k + 6, s7 = k + 7;
   u32 kv = threadIdx.x + k;
   u32 v0 = kv, v1 = kv + 1, v2 = kv + 2, v3 = kv + 3, v4 = kv + 4, v5 = kv + 5, v6 = kv + 6, v7 = kv + 7;
   __syncthreads();
-  const u64 t0 = __builtin_amdgcn_s_memtime();
-  for (int i = 0; i < kIters; ++i) {
+  const u64 t0 = memtime();
+  for (int i = 0; i < iters; ++i) {
     if (MODE == SALU) { S8("s_add_u32"); S8("s_xor_b32"); S8("s_add_u32"); S8("s_xor_b32"); }
     if (MODE == VALU) { V8("v_add_u32"); V8("v_xor_b32"); V8("v_add_u32"); V8("v_xor_b32"); }
     if (MODE == MIX) { S8("s_add_u32"); V8("v_add_u32"); S8("s_xor_b32"); V8("v_xor_b32"); }
     if (MODE == MIX2) { S8("s_add_u32"); V8("v_add_u32"); V8("v_xor_b32"); V8("v_add_u32");
                         S8("s_xor_b32"); V8("v_xor_b32"); }
   }
-  const u64 t1 = __builtin_amdgcn_s_memtime();
+  const u64 t1 = memtime();
   if ((threadIdx.x & 63) == 0) cycles[blockIdx.x * 16 + (threadIdx.x >> 6)] = t1 - t0;
   out[blockIdx.x * blockDim.x + threadIdx.x] = s0 ^ s1 ^ s2 ^ s3 ^ s4 ^ s5 ^ s6 ^ s7 ^ v0 ^ v1 ^ v2 ^ v3 ^ v4 ^ v5 ^ v6 ^ v7;
 }
@@ -57,9 +63,17 @@ __global__ __launch_bounds__(1024) void probe(u32 k, u64* cycles, u32* out) {
 template <int MODE>
 void run(int waves, u64* d_cyc, u32* d_out, u64* h_cyc) {
   const int blocks = 256;
-  probe<MODE><<<blocks, waves * 64>>>(3, d_cyc, d_out);
-  probe<MODE><<<blocks, waves * 64>>>(3, d_cyc, d_out);
-  hipDeviceSynchronize();
+  probe<MODE><<<blocks, waves * 64>>>(3, d_cyc, d_out, kIters);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  const int big = 40 * kIters;
+  hipEventRecord(e0);
+  probe<MODE><<<blocks, waves * 64>>>(3, d_cyc, d_out, big);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0;
+  hipEventElapsedTime(&ms, e0, e1);
   hipMemcpy(h_cyc, d_cyc, sizeof(u64) * blocks * 16, hipMemcpyDeviceToHost);
   u64 mx = 0, sum = 0;
   for (int b = 0; b < blocks; ++b)
@@ -69,12 +83,14 @@ void run(int waves, u64* d_cyc, u32* d_out, u64* h_cyc) {
     }
   const double s_per_wave = MODE == VALU ? 0 : (MODE == MIX2 ? 16.0 : (MODE == MIX ? 16.0 : 32.0)) * kIters;
   const double v_per_wave = MODE == SALU ? 0 : (MODE == MIX2 ? 32.0 : (MODE == MIX ? 16.0 : 32.0)) * kIters;
-  const double avg = (double)sum / (blocks * waves);
-  // s_memtime ticks at the shader clock on gfx950 (checked against events below)
+  const double avg = (double)sum / (blocks * waves) / 40.0;  // per kIters
+  // event time -> instructions per ns per CU (2.4 GHz shader clock: / 2.4 per cycle)
+  const double ns = ms * 1e6;
+  const double s_ns = waves * s_per_wave * 40.0 / ns, v_ns = waves * v_per_wave * 40.0 / ns;
+  // cycles: s_memtime ticks (rate checked against events below)
   printf("{\"mode\": \"%s\", \"waves_per_cu\": %d, \"cycles_max\": %llu, \"cycles_avg\": %.0f, "
-         "\"salu_per_cu_cycle\": %.3f, \"valu_per_cu_cycle\": %.3f, \"cycles_per_wave_instr\": %.2f}\n",
-         kNames[MODE], waves, (unsigned long long)mx, avg, waves * s_per_wave / avg, waves * v_per_wave / avg,
-         avg / (s_per_wave + v_per_wave));
+         "\"event_ms\": %.4f, \"salu_per_cu_ns\": %.3f, \"valu_per_cu_ns\": %.3f, \"memtime_ticks_per_wave_instr\": %.3f}\n",
+         kNames[MODE], waves, (unsigned long long)mx, avg, ms, s_ns, v_ns, avg / (s_per_wave + v_per_wave));
 }
 
 int main() {
@@ -93,7 +109,7 @@ int main() {
   hipEventCreate(&a);
   hipEventCreate(&b);
   hipEventRecord(a);
-  probe<SALU><<<256, 64>>>(3, d_cyc, d_out);
+  probe<SALU><<<256, 64>>>(3, d_cyc, d_out, 40 * kIters);
   hipEventRecord(b);
   hipEventSynchronize(b);
   float ms = 0;
