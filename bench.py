@@ -562,11 +562,39 @@ def end_to_end(torch, codec, op, batch, d_comp, c_off, comp_len, raw_total, comp
         ms = [e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2]), e[2].elapsed_time(e[3])]
         if best is None or sum(ms) < sum(best):
             best = ms
+    # the same H2D timed by the host clock around a synchronize (DESIGN.md
+    # section 5: the event-timed figure above reads 24 GB/s in this process)
+    walls = []
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d_in.copy_(h_in, non_blocking=True)
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+    # where the slow H2D comes from: the same destination from a pinned buffer
+    # filled on the host, and the same source into a fresh device buffer
+    def h2d_rate(dst, src):
+        bestw = 1e9
+        for _ in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            bestw = min(bestw, time.perf_counter() - t0)
+        return round(src.numel() / bestw / 1e9, 2)
+    h_fill = torch.empty(h_in.numel(), dtype=torch.uint8, pin_memory=True)
+    h_fill.fill_(3)
+    d_fresh = torch.empty(h_in.numel(), dtype=torch.uint8, device=dev)
+    h2d_diag = {"host_filled_src": h2d_rate(d_in, h_fill), "fresh_dst": h2d_rate(d_fresh, h_in),
+                "host_filled_src_fresh_dst": h2d_rate(d_fresh, h_fill)}
+    del h_fill, d_fresh
     tot = sum(best) / 1e3
     out = {
         "gib_s_uncompressed": round(raw_total / tot / GIB, 3),
         "h2d_ms": round(best[0], 3), "kernel_ms": round(best[1], 3), "d2h_ms": round(best[2], 3),
         "h2d_gb_s": round(in_bytes / (best[0] / 1e3) / 1e9, 2),
+        "h2d_gb_s_host_clock": round(in_bytes / min(walls) / 1e9, 2),
+        "h2d_gb_s_diag": h2d_diag,
         "d2h_gb_s": round(out_bytes / (best[2] / 1e3) / 1e9, 2),
         "note": "serial pinned hipMemcpyAsync H2D + kernel + D2H on one stream, no overlap",
     }
