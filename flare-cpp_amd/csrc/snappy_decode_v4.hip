@@ -519,6 +519,7 @@ __device__ __forceinline__ i32 index_big_message(
     // steps from this lane.  A 64-byte window holds <= 32 tags (>= 2 bytes
     // each), so 5 rounds cover any chain.
     u32 J = (bad_local || adv >= 64 - lane || nxt >= n_in) ? 64u : lane + adv;
+    const u32 first = ip - wb;
     u64 M = 1ull << lane;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
@@ -531,7 +532,6 @@ __device__ __forceinline__ i32 index_big_message(
         J = Jj;
       }
     }
-    const u32 first = ip - wb;
     const u64 S = ((u64)readlane((u32)(M >> 32), first) << 32) | readlane((u32)M, first);
     const bool in_s = (S >> lane) & 1ull;
     // output position of each chain tag: op + exclusive prefix sum of lengths
@@ -646,6 +646,9 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
 // global-to-global, 1 KiB per instruction.
 // ===========================================================================
 namespace {
+#ifndef FSG_FLUSH_LAG
+#define FSG_FLUSH_LAG 1
+#endif
 #ifndef FSG_FAR_SC1
 #define FSG_FAR_SC1 1
 #endif
@@ -938,6 +941,9 @@ __device__ __forceinline__ void exec_message(
     // ---------- slide the window if this group would overrun it
     if (op + tot_len - sbase > kWindow) {
       const int nsb = (int)(((op - kKeep + obal) & ~15u)) - (int)obal;
+#if FSG_FLUSH_LAG
+      if ((int)flushed < nsb) flush_to((u32)((int)((op + obal) & ~15u) - (int)obal));
+#endif
       const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
       for (u32 k = 0; k < keep; k += 1024) {
         const u32 i = k + 16 * lane;
@@ -989,7 +995,14 @@ __device__ __forceinline__ void exec_message(
     // in flight (far sources lie before the window: flushed long ago)
     {
       const int fe = (int)((op + obal) & ~15u) - (int)obal;
+#if FSG_FLUSH_LAG
+      // once a wave instruction's worth (1 KiB) is complete: every lane
+      // stores a full block.  A slide first flushes what it would drop, so
+      // far sources (below the window base) are always in global memory.
+      if (fe >= (int)flushed + 1024) flush_to((u32)fe);
+#else
       if (fe > (int)flushed) flush_to((u32)fe);
+#endif
     }
     if (global_src) {
       if (kT == 2) xa = expand_pattern(xa, offT, sel_tab);
