@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "../../include/flare_lz4_gpu.h"
 #include "../../include/flare_snappy_gpu.h"
 #include "snappy_device.h"
 
@@ -37,6 +38,12 @@ hipError_t launch_encode(const u8* in, const u64* in_off, const u32* in_len,
                          u32* out_len, i32* status, hipStream_t stream);
 hipError_t launch_gather_blocks(const u64* src, const u32* len, const u64* dst_off, u32 n, u8* dst,
                                 hipStream_t stream);
+size_t lz4_compress_workspace_bytes(u32 n_msgs);
+hipError_t launch_lz4_encode(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u8* out,
+                             const u64* out_off, u32* out_len, i32* status, void* ws, hipStream_t stream);
+hipError_t launch_lz4_decode(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u8* out,
+                             const u64* out_off, const u32* out_cap, u32* out_len, i32* status,
+                             hipStream_t stream);
 }  // namespace fsg
 
 namespace {
@@ -208,6 +215,32 @@ int fsg_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
   return record(fsg::launch_decode_v3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
                                       d_out_cap, d_out_len, d_status, flags, (hipStream_t)stream),
                 "fsg_decompress_batch");
+}
+
+// ---- LZ4 (include/flare_lz4_gpu.h)
+size_t fsg_lz4_max_compressed_length(size_t n) { return 5 + n + n / 255 + 16; }
+
+size_t fsg_lz4_compress_workspace_bytes(uint32_t n_msgs) { return fsg::lz4_compress_workspace_bytes(n_msgs); }
+
+int fsg_lz4_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                           uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off, uint32_t* d_out_len,
+                           int32_t* d_status, void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len || !d_status ||
+                 !d_workspace || workspace_bytes < fsg::lz4_compress_workspace_bytes(n_msgs)))
+    return FSG_ERR_INVALID_ARG;
+  return record(fsg::launch_lz4_encode(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_len, d_status,
+                                       d_workspace, (hipStream_t)stream),
+                "fsg_lz4_compress_batch");
+}
+
+int fsg_lz4_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                             uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off,
+                             const uint32_t* d_out_cap, uint32_t* d_out_len, int32_t* d_status, void* stream) {
+  if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_cap || !d_out_len || !d_status))
+    return FSG_ERR_INVALID_ARG;
+  return record(fsg::launch_lz4_decode(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                       d_status, (hipStream_t)stream),
+                "fsg_lz4_decompress_batch");
 }
 
 }  // extern "C"

@@ -5,6 +5,8 @@
 
 #include "../../include/flare_snappy_host.h"
 #include "gpu_codec.h"
+#include "lz4_compress.h"
+#include "lz4_cpu.h"
 #include "snappy.h"
 #include "snappy_cpu.h"
 
@@ -81,5 +83,19 @@ size_t fsh_cpu_uncompress_as_much(const uint8_t* in, size_t n, size_t frag, uint
   *got = k;
   return r;
 }
+
+size_t fsh_lz4_max_compressed_length(size_t n) { return flare::lz4::cpu::MaxCompressedLength(n); }
+
+size_t fsh_cpu_lz4_compress(const uint8_t* in, size_t n, uint8_t* out) { return flare::lz4::cpu::Compress(in, n, out); }
+
+int fsh_cpu_lz4_uncompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap, uint32_t* ulen) {
+  *ulen = 0;
+  const size_t h = flare::lz4::cpu::ReadHeader(in, n, ulen);
+  if (h == 0) return -1;
+  if (*ulen > cap) return -2;
+  return flare::lz4::cpu::DecompressBlock(in + h, n - h, out, *ulen) ? 1 : 0;
+}
+
+int fsh_register_lz4(void) { return flare::rpc::GlobalInitializeLz4(); }
 
 }  // extern "C"

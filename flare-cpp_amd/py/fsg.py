@@ -17,6 +17,7 @@ PKG_DIR = Path(__file__).resolve().parents[1]
 LIB_DIR = PKG_DIR / "lib"
 REPO_DIR = PKG_DIR.parent
 HEADER = REPO_DIR / "include" / "flare_snappy_gpu.h"
+HEADERS = (HEADER, REPO_DIR / "include" / "flare_lz4_gpu.h")
 
 FSG_OK, FSG_CORRUPT, FSG_BAD_HEADER, FSG_SLOT_TOO_SMALL = 0, 1, 2, 3
 FSG_FLAG_VALIDATE_ONLY, FSG_FLAG_STRICT_HEADER = 1, 2
@@ -37,13 +38,18 @@ _SIGS = {
     "fsg_decompress_workspace_bytes": (_sz, [_u32, _u64]),
     "fsg_compress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "fsg_decompress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
+    "fsg_lz4_max_compressed_length": (_sz, [_sz]),
+    "fsg_lz4_compress_workspace_bytes": (_sz, [_u32]),
+    "fsg_lz4_compress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "fsg_lz4_decompress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 
-def header_symbols(header: Path = HEADER) -> list[str]:
-    """Every fsg_* function declared in include/flare_snappy_gpu.h."""
+def header_symbols(header: Path | None = None) -> list[str]:
+    """Every fsg_* function declared in include/flare_snappy_gpu.h and
+    include/flare_lz4_gpu.h (or in `header`)."""
     import re
-    text = header.read_text()
+    text = "".join(h.read_text() for h in ((header,) if header else HEADERS))
     return sorted(set(re.findall(r"\b(fsg_[a-z0-9_]+)\s*\(", text)))
 
 
@@ -117,6 +123,24 @@ class SnappyGPU:
             _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off),
             _ptr(d_out_cap), _ptr(d_out_len), _ptr(d_status), flags, _ptr(workspace), ws,
             self._stream(stream)), "fsg_decompress_batch")
+
+    # ---- LZ4 (include/flare_lz4_gpu.h)
+    def lz4_compress_workspace(self, n, device=None):
+        import torch
+        nbytes = self.lib.fsg_lz4_compress_workspace_bytes(n)
+        return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device or f"cuda:{self.device}")
+
+    def lz4_compress(self, d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_len, d_status, workspace,
+                     stream=None):
+        self._check(self.lib.fsg_lz4_compress_batch(
+            _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off), _ptr(d_out_len),
+            _ptr(d_status), _ptr(workspace), workspace.numel(), self._stream(stream)), "fsg_lz4_compress_batch")
+
+    def lz4_decompress(self, d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len, d_status,
+                       stream=None):
+        self._check(self.lib.fsg_lz4_decompress_batch(
+            _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off), _ptr(d_out_cap),
+            _ptr(d_out_len), _ptr(d_status), self._stream(stream)), "fsg_lz4_decompress_batch")
 
     def uncompressed_lengths(self, d_in, d_in_off, d_in_len, n, d_ulen, lenient=True, stream=None):
         self._check(self.lib.fsg_uncompressed_lengths_batch(

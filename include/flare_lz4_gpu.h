@@ -1,0 +1,62 @@
+/*
+ * flare_lz4_gpu.h -- batched LZ4 block codec on MI355X (gfx950), in
+ * libflare_snappy_gpu.so next to the Snappy calls (include/flare_snappy_gpu.h:
+ * same batch layout, same status words, same fsg_init / fsg_last_error).
+ *
+ * Reference interface: none to replace.  The reference names
+ * COMPRESS_TYPE_LZ4 = 4 (flare/rpc/options.proto:74) but registers no
+ * handler for it (flare/rpc/compress.cc:26-103 holds only what
+ * RegisterCompressHandler is given; flare/rpc/global.cc:372-376 registers
+ * Snappy/gzip/zlib).  These calls and host/lz4_compress.cc are the handler a
+ * maintainer would register at that slot.
+ *
+ * RPC body (our definition): varint32 of the uncompressed length, then one
+ * LZ4 block.  Blocks are byte-equal to LZ4 1.9.x LZ4_compress_default; the
+ * decoder accepts exactly the blocks LZ4_decompress_safe(dst capacity =
+ * uncompressed length) accepts, except a match of offset 0 (rejected here).
+ */
+#ifndef FLARE_LZ4_GPU_H_
+#define FLARE_LZ4_GPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "flare_snappy_gpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Output slot size of one body: 5 (header) + LZ4_compressBound(n). */
+size_t fsg_lz4_max_compressed_length(size_t n);
+
+/* Device workspace for fsg_lz4_compress_batch: 16 KiB of position table
+ * per message. */
+size_t fsg_lz4_compress_workspace_bytes(uint32_t n_msgs);
+
+/* Batched compress: message i is d_in[d_in_off[i] .. +d_in_len[i]); its body
+ * is written to d_out[d_out_off[i] ..] (slot of
+ * fsg_lz4_max_compressed_length(d_in_len[i]) bytes, slots disjoint);
+ * d_out_len[i] = body length, d_status[i] FSG_OK (FSG_CORRUPT above
+ * 0x7E000000 input bytes, LZ4_MAX_INPUT_SIZE). */
+int fsg_lz4_compress_batch(const uint8_t *d_in, const uint64_t *d_in_off,
+                           const uint32_t *d_in_len, uint32_t n_msgs,
+                           uint8_t *d_out, const uint64_t *d_out_off,
+                           uint32_t *d_out_len, int32_t *d_status,
+                           void *d_workspace, size_t workspace_bytes,
+                           void *stream);
+
+/* Batched decompress: bodies in, d_out[d_out_off[i] ..] with capacity
+ * d_out_cap[i]; d_out_len[i] = the header's length; d_status[i]: FSG_OK,
+ * FSG_CORRUPT, FSG_BAD_HEADER (varint32, at most 5 bytes), or
+ * FSG_SLOT_TOO_SMALL. */
+int fsg_lz4_decompress_batch(const uint8_t *d_in, const uint64_t *d_in_off,
+                             const uint32_t *d_in_len, uint32_t n_msgs,
+                             uint8_t *d_out, const uint64_t *d_out_off,
+                             const uint32_t *d_out_cap, uint32_t *d_out_len,
+                             int32_t *d_status, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLARE_LZ4_GPU_H_ */

@@ -81,6 +81,18 @@ int fsh_cpu_is_valid(const uint8_t* in, size_t n);
 size_t fsh_cpu_uncompress_as_much(const uint8_t* in, size_t n, size_t frag, uint8_t* out,
                                   size_t cap, size_t* got);
 
+/* ---- LZ4 (host/lz4_cpu.h; COMPRESS_TYPE_LZ4, options.proto:74, has no
+ * reference handler): body = varint32 length + one LZ4 block. */
+/* body bound: 5 + LZ4_compressBound(n) */
+size_t fsh_lz4_max_compressed_length(size_t n);
+/* body of n bytes into out; its length (0 above 0x7E000000 bytes) */
+size_t fsh_cpu_lz4_compress(const uint8_t* in, size_t n, uint8_t* out);
+/* body to out (cap bytes): 1 ok, 0 corrupt, -1 bad header, -2 above cap;
+ * *ulen = the header's length when it parses */
+int fsh_cpu_lz4_uncompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap, uint32_t* ulen);
+/* registers the LZ4 CompressHandler (host/lz4_compress.h); 0 on success */
+int fsh_register_lz4(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -156,3 +156,50 @@ class Reference:
                                 out.ctypes.data, out_offs.ctypes.data,
                                 out_caps.ctypes.data if out_caps is not None else None,
                                 out_lens.ctypes.data, threads, frag)
+
+
+LZ4_ORACLE_LIB = ORACLE_DIR / "liboracle_lz4.so"
+
+
+class Lz4Oracle:
+    """The LZ4 block restatement (oracle/liboracle_lz4.so).  RPC body = varint32
+    uncompressed length + one LZ4 block."""
+
+    def __init__(self, path: Path = LZ4_ORACLE_LIB):
+        if not Path(path).exists():
+            raise RuntimeError(f"oracle library missing: {path}")
+        L = ctypes.CDLL(str(path))
+        L.lz4o_max_compressed_length.argtypes = [_sz]
+        L.lz4o_max_compressed_length.restype = _sz
+        L.lz4o_compress_block.argtypes = [_vp, _sz, _vp]
+        L.lz4o_compress_block.restype = _sz
+        L.lz4o_decompress_block.argtypes = [_vp, _sz, _vp, _sz]
+        L.lz4o_compress.argtypes = [_vp, _sz, _vp]
+        L.lz4o_compress.restype = _sz
+        L.lz4o_decompress.argtypes = [_vp, _sz, _vp, _sz, _c.POINTER(_u32)]
+        self.L = L
+
+    def bound(self, n: int) -> int:
+        return self.L.lz4o_max_compressed_length(n)
+
+    def compress_block(self, data: bytes) -> bytes:
+        out = ctypes.create_string_buffer(self.bound(len(data)) + 1)
+        n = self.L.lz4o_compress_block(_buf(data), len(data), out)
+        return out.raw[:n]
+
+    def decompress_block(self, block: bytes, ulen: int):
+        out = ctypes.create_string_buffer(max(ulen, 1))
+        ok = self.L.lz4o_decompress_block(_buf(block), len(block), out, ulen)
+        return bool(ok), (out.raw[:ulen] if ok else None)
+
+    def compress(self, data: bytes) -> bytes:
+        out = ctypes.create_string_buffer(self.bound(len(data)) + 6)
+        n = self.L.lz4o_compress(_buf(data), len(data), out)
+        return out.raw[:n]
+
+    def uncompress(self, body: bytes, cap: int = 1 << 30):
+        """(status, ulen, bytes): status 1 ok, 0 corrupt, -1 bad header, -2 above cap."""
+        ulen = _u32(0)
+        out = ctypes.create_string_buffer(max(min(cap, 1 << 30), 1))
+        r = self.L.lz4o_decompress(_buf(body), len(body), out, cap, ctypes.byref(ulen))
+        return r, ulen.value, (out.raw[:ulen.value] if r == 1 else None)

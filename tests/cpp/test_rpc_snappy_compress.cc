@@ -21,6 +21,7 @@
 #include "compress.h"
 #include "cord_buf.h"
 #include "gpu_codec.h"
+#include "lz4_compress.h"
 #include "snappy.h"
 #include "snappy_compress.h"
 #include "snappy_message.h"
@@ -101,6 +102,33 @@ TEST_CPU(registry_semantics) {
   snappy_message::SnappyMessageProto m2;
   ASSERT_TRUE(ParseFromCompressedData(b, &m2, COMPRESS_TYPE_NONE));
   ASSERT_EQ(m2.text(), "plain");
+}
+
+// COMPRESS_TYPE_LZ4 (options.proto:74): no reference handler; ours on the
+// host codec.  Known answer: varint(200) + liblz4 1.9.3's block of the
+// reference tests' 200-byte text loop.
+TEST_CPU(lz4_handler) {
+  ASSERT_EQ(GlobalInitializeLz4(), 0);
+  ASSERT_EQ(std::string(CompressTypeToCStr(COMPRESS_TYPE_LZ4)), "lz4");
+  ASSERT_TRUE(FindCompressHandler(COMPRESS_TYPE_LZ4) != nullptr);
+  cord_buf in, out, back;
+  in.append(pattern(200, true));
+  ASSERT_TRUE(policy::Lz4Compress(in, &out));
+  ASSERT_EQ(hex(out.to_string()),
+            "c801ff156162636465666768696a6b6c6d6e6f707172737475767778797a3031323334353637383924008c507071727374");
+  ASSERT_TRUE(policy::Lz4Decompress(out, &back));
+  ASSERT_EQ(back.to_string(), pattern(200, true));
+  snappy_message::SnappyMessageProto m, m2;
+  m.set_text(pattern(12435, true));
+  for (int i = 0; i < 3; ++i) m.add_numbers(i * 7);
+  cord_buf b;
+  ASSERT_TRUE(SerializeAsCompressedData(m, &b, COMPRESS_TYPE_LZ4));
+  ASSERT_TRUE(ParseFromCompressedData(b, &m2, COMPRESS_TYPE_LZ4));
+  ASSERT_EQ(m2.text(), m.text());
+  ASSERT_EQ(m2.numbers_size(), 3);
+  cord_buf bad;
+  bad.append(std::string("\x05\x50hel", 5));  // literals cut short
+  ASSERT_FALSE(policy::Lz4Decompress(bad, &back));
 }
 
 TEST_CPU(cord_buf_blocks) {

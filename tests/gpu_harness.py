@@ -66,3 +66,38 @@ class GpuCodec:
         st = d_st.cpu().numpy()[:n]
         outs = [out[int(oo[i]):int(oo[i]) + int(min(ol[i], caps[i]))].tobytes() for i in range(n)]
         return outs, ol, st
+
+    # ---- LZ4 bodies (include/flare_lz4_gpu.h)
+    def lz4_compress(self, batch: fsg.Batch):
+        torch = self.torch
+        n = len(batch)
+        caps = np.array([self.codec.lib.fsg_lz4_max_compressed_length(int(x)) for x in batch.lens], dtype=np.uint64)
+        oo, tot = fsg.slot_offsets(caps)
+        d_out = torch.zeros(tot, dtype=torch.uint8, device="cuda")
+        d_ol = empty(n, torch.int32)
+        d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
+        ws = self.codec.lz4_compress_workspace(n)
+        self.codec.lz4_compress(dev(batch.data), dev(batch.offsets), dev(batch.lens), n, d_out, dev(oo), d_ol, d_st,
+                                ws)
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+        ol = d_ol.cpu().numpy()[:n].view(np.uint32)
+        st = d_st.cpu().numpy()[:n]
+        return [out[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() for i in range(n)], st
+
+    def lz4_decompress(self, bodies: list[bytes], caps: list[int]):
+        torch = self.torch
+        b = fsg.Batch.from_list(bodies)
+        n = len(b)
+        caps = np.array(caps, dtype=np.uint32)
+        oo, tot = fsg.slot_offsets(caps.astype(np.uint64))
+        d_out = torch.zeros(tot, dtype=torch.uint8, device="cuda")
+        d_ol = empty(n, torch.int32)
+        d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
+        self.codec.lz4_decompress(dev(b.data), dev(b.offsets), dev(b.lens), n, d_out, dev(oo), dev(caps), d_ol, d_st)
+        torch.cuda.synchronize()
+        out = d_out.cpu().numpy()
+        ol = d_ol.cpu().numpy()[:n].view(np.uint32)
+        st = d_st.cpu().numpy()[:n]
+        outs = [out[int(oo[i]):int(oo[i]) + int(min(ol[i], caps[i]))].tobytes() for i in range(n)]
+        return outs, ol, st
