@@ -23,6 +23,26 @@ namespace fsg {
 
 namespace {
 
+// The block codec is __host__ __device__ so tools/lz4_host_check.hip can run
+// it on the CPU (under AddressSanitizer) against the oracle.
+#define LZ4_HD __host__ __device__ __forceinline__
+
+LZ4_HD u32 ld32(const u8* p) {
+  u32 v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
+LZ4_HD u64 ld64(const u8* p) {
+  u64 v;
+  __builtin_memcpy(&v, p, 8);
+  return v;
+}
+LZ4_HD void cp16(u8* d, const u8* s) {
+  u32x4 v;
+  __builtin_memcpy(&v, s, 16);
+  __builtin_memcpy(d, &v, 16);
+}
+
 constexpr u32 kLz4MinMatch = 4;
 constexpr u32 kLz4MfLimit = 12;
 constexpr u32 kLz4LastLiterals = 5;
@@ -33,29 +53,29 @@ constexpr u32 kLz4Limit64K = 65536 + kLz4MfLimit - 1;
 constexpr u32 kLz4MaxInput = 0x7E000000u;  // LZ4_MAX_INPUT_SIZE
 constexpr u32 kLz4TableBytes = 16384;       // either table: 8,192 x u16 or 4,096 x u32
 
-__device__ __forceinline__ u32 lz4_hash(const u8* p, bool small) {
-  if (small) return (ldu32(p) * 2654435761u) >> (32 - (kLz4HashLog + 1));
-  return (u32)(((ldu64(p) << 24) * 889523592379ull) >> (64 - kLz4HashLog));
+LZ4_HD u32 lz4_hash(const u8* p, bool small) {
+  if (small) return (ld32(p) * 2654435761u) >> (32 - (kLz4HashLog + 1));
+  return (u32)(((ld64(p) << 24) * 889523592379ull) >> (64 - kLz4HashLog));
 }
 
 // n bytes from s to d, 16 at a time then singly (never past d + n)
-__device__ __forceinline__ void copy_exact(u8* d, const u8* s, u32 n) {
+LZ4_HD void copy_exact(u8* d, const u8* s, u32 n) {
   u32 k = 0;
-  for (; k + 16 <= n; k += 16) copy16(d + k, s + k);
+  for (; k + 16 <= n; k += 16) cp16(d + k, s + k);
   for (; k < n; ++k) d[k] = s[k];
 }
 
-__device__ __forceinline__ u8* put_length(u8* op, u32 len) {
+LZ4_HD u8* put_length(u8* op, u32 len) {
   for (; len >= 255; len -= 255) *op++ = 255;
   *op++ = (u8)len;
   return op;
 }
 
 // count of equal bytes at a[i], b[i] with a + i < limit (LZ4_count)
-__device__ __forceinline__ u32 match_count(const u8* a, const u8* b, const u8* limit) {
+LZ4_HD u32 match_count(const u8* a, const u8* b, const u8* limit) {
   u32 c = 0;
   while (a + c + 8 <= limit) {
-    const u64 x = ldu64(a + c) ^ ldu64(b + c);
+    const u64 x = ld64(a + c) ^ ld64(b + c);
     if (x) return c + ((u32)__builtin_ctzll(x) >> 3);
     c += 8;
   }
@@ -64,7 +84,7 @@ __device__ __forceinline__ u32 match_count(const u8* a, const u8* b, const u8* l
 }
 
 // One block (the oracle's lz4o_compress_block); returns bytes written.
-__device__ u32 lz4_compress_block(const u8* src, u32 n, u8* dst, u8* table) {
+__host__ __device__ u32 lz4_compress_block(const u8* src, u32 n, u8* dst, u8* table) {
   const bool small = n < kLz4Limit64K;
   u16* t16 = reinterpret_cast<u16*>(table);
   u32* t32 = reinterpret_cast<u32*>(table);
@@ -96,7 +116,7 @@ __device__ u32 lz4_compress_block(const u8* src, u32 n, u8* dst, u8* table) {
           fh = lz4_hash(src + fwd, small);
           put(h, cur);
           if (!small && mi + kLz4DistanceMax < cur) continue;  // too far
-          if (ldu32(src + match) == ldu32(src + ip)) break;
+          if (ld32(src + match) == ld32(src + ip)) break;
         }
       }
       while (ip > anchor && match > 0 && src[ip - 1] == src[match - 1]) {  // extend backwards
@@ -133,7 +153,7 @@ __device__ u32 lz4_compress_block(const u8* src, u32 n, u8* dst, u8* table) {
         put(lz4_hash(src + ip - 2, small), ip - 2);
         const u32 h = lz4_hash(src + ip, small), mi = get(h);
         put(h, ip);
-        if ((small || mi + kLz4DistanceMax >= ip) && ldu32(src + mi) == ldu32(src + ip)) {
+        if ((small || mi + kLz4DistanceMax >= ip) && ld32(src + mi) == ld32(src + ip)) {
           match = mi;
           token = op++;
           *token = 0;
@@ -160,7 +180,7 @@ last_literals : {
 
 // One block to exactly ulen bytes (the oracle's lz4o_decompress_block):
 // true when valid.
-__device__ bool lz4_decompress_block(const u8* src, u32 n, u8* dst, u32 ulen) {
+__host__ __device__ bool lz4_decompress_block(const u8* src, u32 n, u8* dst, u32 ulen) {
   u32 ip = 0, op = 0;
   for (;;) {
     if (ip >= n) return false;
@@ -200,7 +220,8 @@ __device__ bool lz4_decompress_block(const u8* src, u32 n, u8* dst, u32 ulen) {
     if (off >= 16) {
       copy_exact(d, d - off, ml);  // each 16-byte step reads bytes already written
     } else {
-      for (u32 k = 0; k < ml; ++k) d[k] = d[k - off];
+      const u8* from = d - off;  // overlapping: byte by byte, in order
+      for (u32 k = 0; k < ml; ++k) d[k] = from[k];
     }
     op += ml;
   }

@@ -190,7 +190,8 @@ bool DecompressBlock(const uint8_t* in, size_t n, uint8_t* out, size_t ulen) {
     if (off >= len) {
       std::memcpy(d, d - off, len);
     } else {
-      for (size_t k = 0; k < len; ++k) d[k] = d[k - off];
+      const uint8_t* from = d - off;  // overlapping: byte by byte, in order
+      for (size_t k = 0; k < len; ++k) d[k] = from[k];
     }
     op += len;
   }

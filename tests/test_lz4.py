@@ -138,3 +138,68 @@ def test_host_codec_verdicts_equal_oracle(host, o):
         want = o.uncompress(b, cap=1 << 15)
         got = _host_uncompress(host, b, 1 << 15)
         assert got[0] == want[0] and (want[0] != 1 or got[2] == want[2]), i
+
+
+# ---- the GPU kernels' block codec on the CPU under AddressSanitizer
+# (tests/cpp/lz4_host_check.hip includes csrc/lz4.hip; its block functions are
+# __host__ __device__), so an out-of-bounds access shows up without a GPU.
+
+@pytest.fixture(scope="module")
+def host_check(tmp_path_factory):
+    import shutil
+    import subprocess
+    repo = Path(__file__).resolve().parents[1]
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not Path(hipcc).exists():
+        pytest.skip("hipcc not available")
+    exe = tmp_path_factory.mktemp("lz4hc") / "lz4_host_check"
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O1", "-g", "-Xarch_host", "-fsanitize=address",
+                        "-I", str(repo / "flare-cpp_amd" / "csrc"), str(repo / "tests" / "cpp" / "lz4_host_check.hip"),
+                        "-o", str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return exe
+
+
+def _run_check(exe, mode, payload: bytes, tmp_path):
+    import subprocess
+    fin, fout = tmp_path / f"{mode}.in", tmp_path / f"{mode}.out"
+    fin.write_bytes(payload)
+    r = subprocess.run([str(exe), mode, str(fin), str(fout)], capture_output=True, text=True, timeout=300,
+                       env={"ASAN_OPTIONS": "detect_leaks=0"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    return fout.read_bytes()
+
+
+def test_gpu_block_codec_on_host_asan(host_check, o, tmp_path):
+    import struct
+    rng = np.random.default_rng(29)
+    xs = [build_input(v) for v in VEC["compress"] if v["input_len"] <= 300000]
+    for t in range(150):
+        n = int(rng.choice([rng.integers(0, 40), rng.integers(0, 5000), rng.integers(60000, 70000)]))
+        xs.append(rng.integers(0, int(rng.choice([1, 2, 4, 256])), n, dtype=np.uint8).tobytes())
+    out = _run_check(host_check, "c", b"".join(struct.pack("<I", len(x)) + x for x in xs), tmp_path)
+    p = 0
+    for x in xs:
+        (n,) = struct.unpack_from("<I", out, p)
+        p += 4
+        assert out[p:p + n] == o.compress_block(x), len(x)
+        p += n
+    cases = [(d["ulen"], bytes.fromhex(d["hex"])) for d in VEC["decode"]]
+    src = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (40, 900, 20000)]
+    for i in range(2000):
+        b = bytearray(o.compress_block(src[i % 3]))
+        for _ in range(int(rng.integers(1, 3))):
+            b[int(rng.integers(len(b)))] = int(rng.integers(256))
+        if rng.random() < 0.3:
+            b = b[:int(rng.integers(1, len(b) + 1))]
+        cases.append((len(src[i % 3]) if rng.random() < 0.8 else int(rng.integers(0, 30000)), bytes(b)))
+    out = _run_check(host_check, "d", b"".join(struct.pack("<II", u, len(b)) + b for u, b in cases), tmp_path)
+    p = 0
+    for u, b in cases:
+        (ok,) = struct.unpack_from("<i", out, p)
+        p += 4
+        want, y = o.decompress_block(b, u)
+        assert bool(ok) == want
+        if ok:
+            assert out[p:p + u] == y
+            p += u
