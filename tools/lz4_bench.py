@@ -1,0 +1,124 @@
+"""LZ4 leg: device-resident batched LZ4 encode
+and decode of the C3 bodies (65,536 x 64 KiB text), timed with HIP events on
+the launch stream, round trip and an oracle sample checked untimed.  CPU
+lines beside it: the oracle (single thread) and the system liblz4 1.9.3 on a
+sample (checkers only, never the product path).
+
+    python tools/lz4_bench.py [--n 65536] [--size 65536] [--steps 5]
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+for p in (REPO / "flare-cpp_amd" / "py", REPO / "oracle", REPO / "tests"):
+    sys.path.insert(0, str(p))
+import fsg  # noqa: E402
+
+GIB = float(1 << 30)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--size", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=5)
+    a = ap.parse_args()
+    import torch
+    dev = torch.device("cuda", 0)
+    codec = fsg.SnappyGPU(0)
+    lib = codec.lib
+    batch = fsg.make_batch(fsg.KIND_TEXT, np.full(a.n, a.size, np.uint32))
+    n, raw = len(batch), batch.total
+    H = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)  # noqa: E731
+    d_raw, d_ro, d_rl = H(batch.data), H(batch.offsets), H(batch.lens)
+    caps = np.array([lib.fsg_lz4_max_compressed_length(int(x)) for x in batch.lens], np.uint64)
+    c_off, c_tot = fsg.slot_offsets(caps)
+    d_c, d_co = torch.zeros(c_tot, dtype=torch.uint8, device=dev), H(c_off)
+    d_cl = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_st = torch.zeros(n, dtype=torch.int32, device=dev)
+    ws = codec.lz4_compress_workspace(n)
+    d_out = torch.zeros(raw, dtype=torch.uint8, device=dev)
+    d_ol = torch.zeros(n, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream()
+
+    def enc():
+        codec.lz4_compress(d_raw, d_ro, d_rl, n, d_c, d_co, d_cl, d_st, ws, stream=s)
+
+    def dec():
+        codec.lz4_decompress(d_c, d_co, d_cl, n, d_out, d_ro, d_rl, d_ol, d_st, stream=s)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(a.steps):
+            fn()
+        e1.record(s)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / a.steps
+
+    enc_ms = timed(enc)
+    comp_len = d_cl.cpu().numpy().view(np.uint32)
+    comp = int(comp_len.astype(np.uint64).sum())
+    enc_ok = int((d_st != 0).sum().item()) == 0
+    dec_ms = timed(dec)
+    dec_ok = int((d_st != 0).sum().item()) == 0 and bool(torch.equal(d_out, d_raw))
+    from bind import Lz4Oracle
+    o = Lz4Oracle()
+    host_c = d_c.cpu().numpy()
+    idx = np.linspace(0, n - 1, 32).astype(np.int64)
+    sample_ok = all(host_c[int(c_off[i]):int(c_off[i]) + int(comp_len[i])].tobytes() == o.compress(batch.item(int(i)))
+                    for i in idx)
+    # CPU lines on a sample (checkers): oracle and system liblz4, one thread
+    k = min(n, 1024)
+    items = [batch.item(i) for i in range(k)]
+    t = time.perf_counter()
+    blocks = [o.compress_block(x) for x in items]
+    t_oc = time.perf_counter() - t
+    t = time.perf_counter()
+    for x, b in zip(items, blocks):
+        o.decompress_block(b, len(x))
+    t_od = time.perf_counter() - t
+    sysl = None
+    try:
+        from lz4_sys import SysLz4, load
+        L = load()
+        if L is not None:
+            z = SysLz4(L)
+            t = time.perf_counter()
+            for x in items:
+                z.compress(x)
+            t_sc = time.perf_counter() - t
+            t = time.perf_counter()
+            for x, b in zip(items, blocks):
+                z.decompress(b, len(x))
+            t_sd = time.perf_counter() - t
+            kb = sum(map(len, items))
+            sysl = {"compress_gib_s": round(kb / t_sc / GIB, 3), "decompress_gib_s": round(kb / t_sd / GIB, 3),
+                    "cores": 1, "version": z.version}
+    except Exception as e:  # pragma: no cover - diagnostic only
+        sysl = {"error": str(e)}
+    kb = sum(map(len, items))
+    out = {
+        "workload": f"C3 bodies through LZ4: {n} x {a.size} B text, device-resident",
+        "raw_bytes": raw, "compressed_bytes": comp, "ratio": round(raw / comp, 4),
+        "encode": {"ms": round(enc_ms, 3), "gib_s": round(raw / (enc_ms / 1e3) / GIB, 3), "status_ok": enc_ok,
+                   "roofline_frac": round((raw + comp) / (enc_ms / 1e3) / 8e12, 4)},
+        "decode": {"ms": round(dec_ms, 3), "gib_s": round(raw / (dec_ms / 1e3) / GIB, 3), "roundtrip_ok": dec_ok,
+                   "roofline_frac": round((raw + comp) / (dec_ms / 1e3) / 8e12, 4)},
+        "oracle_sample_ok": sample_ok,
+        "cpu_oracle_1thread": {"compress_gib_s": round(kb / t_oc / GIB, 3), "decompress_gib_s": round(kb / t_od / GIB, 3),
+                               "sample": f"first {k} bodies"},
+        "cpu_system_liblz4_1thread": sysl,
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
