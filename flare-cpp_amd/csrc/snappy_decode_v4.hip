@@ -11,9 +11,11 @@
 //   pass 1, index_kernel (one LANE per message): the reference's tag walk
 //     (SnappyDecompressor::DecompressAllTags, /root/reference/flare/io/snappy/
 //     snappy.cc:716-787, with the writer checks of :1141-1227 / :1331-1481)
-//     without touching output.  It produces the final per-message status and
-//     a tag-start bitmap over the compressed bytes (bit p = a tag starts at
-//     compressed offset p), 1/8 of the input size.  Pure VALU + LDS ring
+//     without touching output.  It produces the per-message status (pass 2
+//     adds the copy-offset check, :1200/:1410/:1466, where every tag's output
+//     position is already known) and a tag-start bitmap over the compressed
+//     bytes (bit p = a tag starts at compressed offset p), 1/8 of the input
+//     size.  Pure VALU + LDS ring
 //     reads; each lane reads its own input once.
 //
 //   pass 2, exec_kernel (one WAVE per message, only status-OK messages):
@@ -161,14 +163,15 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
 
   const u32 lane = threadIdx.x & 63;
   // Tag table (the role of char_table, snappy.cc:516-549): per tag byte c,
-  // bits 0-2 extra bytes, 3 long literal, 4 literal, 8-15 advance without a
-  // long literal's length, 16-23 length (short literal / copies), 24-26 a
-  // COPY_1's offset bits 8-10.
+  // bits 0-4 the right shift of 0xffffffff that masks the nb extra bytes
+  // ((32 - 8 nb) & 31: a shift uses the low 5 bits of its operand), 5 long
+  // literal, 8-15 advance without a long literal's length, 16-23 length
+  // (short literal / copies).
   __shared__ u32 tagtab[256];
 #pragma unroll
   for (u32 q = 0; q < 4 / kIdxWaves; ++q) {
     const u32 c = threadIdx.x * (4 / kIdxWaves) + q, type = c & 3, l0 = (c >> 2) + 1;
-    u32 nb, len, lit = 0, ll = 0, hi3 = 0;
+    u32 nb, len, lit = 0, ll = 0;
     if (type == 0) {
       lit = 1;
       nb = l0 > 60 ? l0 - 60 : 0;
@@ -177,13 +180,12 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
     } else if (type == 1) {
       nb = 1;
       len = 4 + ((c >> 2) & 7);
-      hi3 = c >> 5;
     } else {
       nb = type == 2 ? 2 : 4;
       len = l0;
     }
     const u32 adv = 1 + nb + (lit && !ll ? len : 0);
-    tagtab[c] = nb | (ll << 3) | (lit << 4) | (adv << 8) | (len << 16) | (hi3 << 24);
+    tagtab[c] = ((32 - 8 * nb) & 31) | (ll << 5) | (adv << 8) | (len << 16);
   }
   __syncthreads();
   const bool strict = flags & 2u;
@@ -343,29 +345,31 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
       // offset, masked to their count nb; selects, no exec-mask branches.
       const u32 c = t0 & 0xffu;
       const u32 e = tagtab[c];
-      const u32 nb = e & 7u;
-      const u32 val = ext & (0xffffffffu >> ((32 - 8 * nb) & 31));
-      const bool longlit = (e & 8u) != 0;
-      const u32 len = longlit ? val + 1u : (e >> 16) & 0xffu;  // uint32 wrap: 0xffffffff+1 == 0
-      const u32 type = (e & 16u) ? 0u : 1u;  // 0 = literal (only literal-ness is used below)
+      const u32 val = ext & (0xffffffffu >> (e & 31u));
+      // a long literal's length (uint32 wrap: 0xffffffff+1 == 0, as the
+      // reference's uint32 sum), else the table's (0 for long literals); masks,
+      // not a select, so the compiler keeps the unrolled walk branch-free
+      const u32 llmask = 0u - ((e >> 5) & 1u);
+      const u32 lpart = (val + 1u) & llmask;
+      const u32 len = lpart + ((e >> 16) & 0xffu);
       // The walk advances over every tag below lim whether or not it passed
       // its checks, so the checks stay off the ip -> ip dependency chain.
       // After the first failing tag the status is final (kCorrupt): what the
       // walk reads from there on only sets bits in the LDS ring, which are
       // never stored for a corrupt message, and ring indices are masked.
       const bool look = ip < lim;
-      const u32 nx = ip + ((e >> 8) & 0xffu) + (longlit ? len : 0u);
-      const u32 ip_next = look ? nx : ip;
+      const u32 adv = (e >> 8) & 0xffu;  // tag byte + extra bytes (+ a short literal's bytes)
+      const u32 step = adv + lpart;
+      const u32 ip_next = look ? ip + step : ip;
       if (j + 1 < kIdxTags) ring_read(ip_next, lo, hi);
-      const u32 coff = val | ((e >> 16) & 0x700u);
-      // tag bytes and literal bytes present (:744-761), compared against the
-      // bytes left after the tag so no sum can wrap (a 4-byte literal length
-      // of 0xfffffffa..0xfffffffe would wrap nx back onto its own length
-      // bytes); copy offset in range (:1200, 1410, 1466).  The writer's space
-      // check (:1166, :1400) is per iteration, below: op only grows.
-      const u32 avail = n_in - ip - 1;  // ip < n_in whenever `look`
-      const bool bad = (avail < nb) | ((avail - nb < len) & (type == 0)) |
-                       ((coff - 1u >= op) & (type != 0));
+      // Tag bytes and literal bytes present (:744-761): the step fits the
+      // bytes left (ip < n_in whenever `look`).  A 4-byte literal length can
+      // wrap the u32 step (the true step is >= 2^32 > any input), which shows
+      // as step < adv.  Copy offsets (:1200, :1410, :1466) are checked by the
+      // exec pass, which has every tag's output position at hand (this pass
+      // only feeds it); the writer's space check (:1166, :1400) is per
+      // iteration, below: op only grows.
+      const bool bad = (step > n_in - ip) | (step < adv);
       status = (look && bad) ? kCorrupt : status;
       const bool take = look && !bad;
       // unconditional (bits land in the LDS ring even without a bitmap): a
