@@ -435,3 +435,44 @@ def test_far_copies_at_window_edge(gpu, oracle):
     for i in range(0, 800, 97):
         ok, ulen, ref = oracle.uncompress(comps[i], cap=len(raws[i]))
         assert ok and ref == raws[i], i
+
+
+def test_mutations_and_trailing_tags(gpu, oracle):
+    """Text bodies of 3-60 KB (compressed 1.5-30 KB, the lane index pass),
+    with an incompressible block placed near the middle (a long literal),
+    intact and with 1-3 mutated bytes anywhere, plus tags after the output is
+    complete: a zero-length literal (fc ff ff ff ff) is accepted by the
+    reference, any other tag rejected (writer space, snappy.cc:1166/:1400)."""
+    rng = np.random.default_rng(17)
+    comps = []
+    for n in (3000, 4500, 8000, 20000, 60000):
+        text = fsg.make_batch(fsg.KIND_TEXT, [n], first_index=n).item(0)
+        base = oracle.compress(text)
+        comps.append(base)
+        for frac in (0.35, 0.45, 0.5, 0.55):
+            blk = rng.integers(0, 256, int(rng.choice([100, 300, 1500])), dtype=np.uint8).tobytes()
+            at = int(len(text) * frac)
+            comps.append(oracle.compress(text[:at] + blk + text[at:]))
+        for _ in range(60):
+            c = bytearray(base)
+            for _ in range(int(rng.integers(1, 4))):
+                c[int(rng.integers(len(c)))] = int(rng.integers(256))
+            comps.append(bytes(c))
+        comps.append(base + b"\xfc\xff\xff\xff\xff")
+        comps.append(base + b"\xfc\xff\xff\xff\xff" + b"\xfc\xff\xff\xff\xff")
+        comps.append(base + b"\x00A")
+        comps.append(base + b"\x05\x01")  # COPY_1 len 5 offset 1
+        comps.append(base + b"\xfc\xff\xff\xff\xff\x00A")
+    outs, ol, st = gpu.decompress(comps, [1 << 17] * len(comps))
+    n_ok = n_bad = 0
+    for i, (c, o, s) in enumerate(zip(comps, outs, st)):
+        ok, ulen, ref = oracle.uncompress(c, cap=1 << 17)
+        if ok is None:
+            assert s == fsg.FSG_SLOT_TOO_SMALL, i
+        elif not ok:
+            n_bad += 1
+            assert s in (fsg.FSG_CORRUPT, fsg.FSG_BAD_HEADER), (i, len(c), s)
+        else:
+            n_ok += 1
+            assert s == fsg.FSG_OK and o[:ulen] == ref, (i, len(c), s)
+    assert n_ok > 40 and n_bad > 40
