@@ -21,7 +21,14 @@
 
 namespace fsg {
 
-constexpr int kProbeWindow = 16;  // probes evaluated per wave step
+constexpr int kProbeWindow = 16;  // probes evaluated per wave step: one DPP row
+
+// Lane l of a 16-lane row gets v from lane l - D (ROW_SHR) or l + D (ROW_SHL)
+// of the same row, `old` where that lane is outside the row: one VALU
+// instruction, where a shuffle is an LDS round trip.
+#define FSG_ROW_SHR(old, v, D) ((u32)__builtin_amdgcn_update_dpp((int)(old), (int)(v), 0x110 + (D), 0xf, 0xf, false))
+#define FSG_ROW_SHL(old, v, D) ((u32)__builtin_amdgcn_update_dpp((int)(old), (int)(v), 0x100 + (D), 0xf, 0xf, false))
+#define FSG_REP15(M) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15)
 
 __device__ __forceinline__ u32 wave_bcast(u32 v, int src_lane) {
   return (u32)__builtin_amdgcn_readlane((int)v, src_lane);
@@ -114,11 +121,10 @@ __device__ u64 compress_fragment_wave(const u8* input, u32 n, u8* dst, u64 op,
         // lane k: p_k = ip + sum_{j<k} ((skip + j) >> 5)
         u32 step = (skip + (u32)lane) >> 5;
         u32 incl = step;
-#pragma unroll
-        for (int d = 1; d < kProbeWindow; d <<= 1) {
-          u32 t = __shfl_up(incl, d, kWave);
-          if (lane >= d) incl += t;
-        }
+        incl += FSG_ROW_SHR(0u, incl, 1);
+        incl += FSG_ROW_SHR(0u, incl, 2);
+        incl += FSG_ROW_SHR(0u, incl, 4);
+        incl += FSG_ROW_SHR(0u, incl, 8);
         u32 p = ip + incl - step;
         u32 p_next = p + step;
         // probe k runs iff the following position is still <= ip_limit (:387)
@@ -126,14 +132,13 @@ __device__ u64 compress_fragment_wave(const u8* input, u32 n, u8* dst, u64 op,
         u32 bytes = exec ? ldu32(input + p) : 0u;
         u32 h = hash_bytes(bytes, shift);
         u32 old = exec ? (u32)table[h] : 0u;
-        // latest earlier probe in this window with the same hash
+        // latest earlier probe in this window with the same hash (a probe
+        // that does not run carries a key no hash equals)
+        const u32 hx = exec ? h : (0x40000000u | (u32)lane);
         int prev = -1;
-#pragma unroll
-        for (int d = 1; d < kProbeWindow; ++d) {
-          u32 hd = __shfl_up(h, d, kWave);
-          int ed = __shfl_up((int)exec, d, kWave);
-          if (prev < 0 && lane >= d && ed && hd == h) prev = lane - d;
-        }
+#define FSG_COLL(D) { const u32 hd = FSG_ROW_SHR(0x7fffffffu, hx, D); if (prev < 0 && hd == hx) prev = lane - (D); }
+        FSG_REP15(FSG_COLL)
+#undef FSG_COLL
         u32 pp = __shfl(p, prev < 0 ? lane : prev, kWave);
         u32 cand = prev >= 0 ? pp : old;
         bool match = exec && ldu32(input + cand) == bytes;
@@ -144,11 +149,9 @@ __device__ u64 compress_fragment_wave(const u8* input, u32 n, u8* dst, u64 op,
         else last = em ? 63 - __clzll((long long)em) : -1;
         // commit table[h_k] = p_k for k <= last, last writer per hash wins
         bool later = false;
-#pragma unroll
-        for (int d = 1; d < kProbeWindow; ++d) {
-          u32 hd = __shfl_down(h, d, kWave);
-          if (lane + d <= last && hd == h) later = true;
-        }
+#define FSG_LATER(D) { const u32 hd = FSG_ROW_SHL(0x7fffffffu, hx, D); if (lane + (D) <= last && hd == hx) later = true; }
+        FSG_REP15(FSG_LATER)
+#undef FSG_LATER
         if (exec && lane <= last && !later) table[h] = (u16)p;
         if (mm) {
           ip = wave_bcast(p, last);

@@ -101,14 +101,21 @@ def test_config_digests(gpu, name):
     assert all(o == b.item(i) for i, o in enumerate(outs))
 
 
-def test_randomized_against_oracle(gpu, oracle):
-    rng = np.random.default_rng(3)
+@pytest.mark.parametrize("encoder", [0, 1])
+def test_randomized_against_oracle(gpu, oracle, encoder):
+    """Random-alphabet inputs (0 B to 140 KB): the default encoder and the
+    LDS-table wave encoder (v1, DPP row exchanges) byte-equal to the oracle."""
+    gpu.codec.select_kernels(0, encoder)
+    rng = np.random.default_rng(3 + encoder)
     items = []
-    for t in range(400):
+    for t in range(400 if encoder == 0 else 150):
         n = int(rng.choice([rng.integers(0, 100), rng.integers(0, 5000), rng.integers(0, 140000)]))
         alpha = int(rng.choice([2, 3, 8, 40, 256]))
         items.append(rng.integers(0, alpha, n, dtype=np.uint8).tobytes())
-    comps, st = gpu.compress(fsg.Batch.from_list(items))
+    try:
+        comps, st = gpu.compress(fsg.Batch.from_list(items))
+    finally:
+        gpu.codec.select_kernels(0, 0)
     assert (st == 0).all()
     for x, c in zip(items, comps):
         assert c == oracle.compress(x)
