@@ -39,6 +39,8 @@
 #include "snappy_lane_decode.h"
 #include "snappy_pieces.h"
 
+#include <mutex>
+
 namespace fsg {
 
 namespace {
@@ -1162,6 +1164,31 @@ size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   return (size_t)(256 + kListBases * base_bytes + 4 * words);
 }
 
+// Per-device side stream and fork/join events for launch_decode_v4 (created
+// on first use; the mutex orders each call's record/wait pairs when several
+// host threads decode at once).  nullptr when they cannot be created: the
+// passes then run in one stream.
+struct SideStream {
+  hipStream_t stream = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  std::mutex mu;
+};
+static SideStream* side_stream() {
+  constexpr int kMaxDevices = 64;
+  static SideStream g_side[kMaxDevices];
+  static std::once_flag g_once[kMaxDevices];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+  SideStream* s = &g_side[dev];
+  std::call_once(g_once[dev], [s] {
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&s->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->join, hipEventDisableTiming) != hipSuccess)
+      s->stream = nullptr;
+  });
+  return s->stream ? s : nullptr;
+}
+
 hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u8* out, const u64* out_off,
                             const u32* out_cap, u32* out_len, i32* status,
@@ -1198,28 +1225,68 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
       in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap, cap_words,
       big_count, big_list, big_threshold);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  // pass 1b: large messages, one wave each (an empty list costs one short
-  // launch); they land in pass 2's work lists
-  {
+  // Pass 1b and the large-message exec blocks run on a side stream, after
+  // pass 1 (which lists the large messages) and beside the one-wave-per-
+  // message exec launch: pass 1b is bound by the serial window walk of the
+  // few largest bodies and leaves most CUs idle, which the small messages'
+  // execution fills.  Both streams join before the fallback pass.
+  // Only for batches of > 128K messages (the mixed-size ones): a fork and
+  // join cost ~10 us (C2 0.159 -> 0.169 ms), and uniform batches send nothing
+  // to pass 1b (CM 14.4 -> 12.1 ms).  FSG_DECODE_FORK=0/1 forces (A/B).
+  const u32 small_blocks = (n_msgs + kWavesPerBlock - 1) / kWavesPerBlock;
+  static const u32 kBigBlocks = [] {  // A/B knob
+    // at least one block: the large-message lists are only drained there
+    const char* e = getenv("FSG_EXEC_BIG_BLOCKS");
+    const int v = e ? atoi(e) : 512;
+    return v >= 1 ? (u32)v : 512u;
+  }();
+  const char* fork_env = getenv("FSG_DECODE_FORK");  // read per call: tests set it
+  const bool fork = fork_env ? atoi(fork_env) != 0 : n_msgs > 131072u;
+  const u32 big_blocks = small_blocks < kBigBlocks ? small_blocks : kBigBlocks;
+  auto launch_index_big = [&](hipStream_t st) -> hipError_t {
+    // pass 1b: large messages, one wave each (an empty list costs one short
+    // launch); they land in pass 2's work lists
     const u32 q = (n_msgs + 3) / 4;
     const u32 blocks = q < 1024u ? q : 1024u;
-    index_big_kernel<<<blocks, 256, 0, stream>>>(
+    index_big_kernel<<<blocks, 256, 0, st>>>(
         in, in_off, in_len, out_len, flags, status, bm_base, bitmap, big_count, big_list,
         reinterpret_cast<u32*>(w + 128), n_msgs, out, out_off, seg_list,
         reinterpret_cast<u32*>(w + 160), whole_list, reinterpret_cast<u32*>(w + 224));
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  }
-  {
-    // large-message blocks (exit after one atomic when the lists are empty),
-    // then one wave per message
-    const u32 small_blocks = (n_msgs + kWavesPerBlock - 1) / kWavesPerBlock;
-    static const u32 kBigBlocks = [] {  // A/B knob
-      // at least one block: the large-message lists are only drained there
-      const char* e = getenv("FSG_EXEC_BIG_BLOCKS");
-      const int v = e ? atoi(e) : 512;
-      return v >= 1 ? (u32)v : 512u;
-    }();
-    const u32 big_blocks = small_blocks < kBigBlocks ? small_blocks : kBigBlocks;
+    return hipGetLastError();
+  };
+  auto launch_big = [&](hipStream_t st) -> hipError_t {
+    hipError_t e2 = launch_index_big(st);
+    if (e2 != hipSuccess) return e2;
+    // the large-message blocks only (exit after one atomic when the lists
+    // are empty)
+    exec_kernel<<<big_blocks, kWavesPerBlock * 64, 0, st>>>(
+        in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
+        reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
+        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), big_blocks, big_threshold);
+    return hipGetLastError();
+  };
+  auto launch_small = [&](hipStream_t st) -> hipError_t {
+    // one wave per message; large ones are skipped (big_blocks = 0: no block
+    // takes the large-message role)
+    exec_kernel<<<small_blocks, kWavesPerBlock * 64, 0, st>>>(
+        in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
+        reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
+        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), 0u, big_threshold);
+    return hipGetLastError();
+  };
+  SideStream* side = fork ? side_stream() : nullptr;
+  if (side) {
+    std::lock_guard<std::mutex> lk(side->mu);
+    if ((e = hipEventRecord(side->fork, stream)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(side->stream, side->fork, 0)) != hipSuccess) return e;
+    if ((e = launch_big(side->stream)) != hipSuccess) return e;
+    if ((e = hipEventRecord(side->join, side->stream)) != hipSuccess) return e;
+    if ((e = launch_small(stream)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(stream, side->join, 0)) != hipSuccess) return e;
+  } else {
+    // one stream: pass 1b, then one exec launch whose first blocks take the
+    // large messages (dispatched first) and the rest one message per wave
+    if ((e = launch_index_big(stream)) != hipSuccess) return e;
     exec_kernel<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,

@@ -150,10 +150,15 @@ def test_decode_fuzz_against_oracle(gpu, oracle, variant):
     gpu.codec.select_kernels(0, 0)
 
 
-def test_large_message_index_fuzz(gpu, oracle):
+@pytest.mark.parametrize("fork", ["0", "1"])
+def test_large_message_index_fuzz(gpu, oracle, fork, monkeypatch):
     """Compressed bodies over 48 KiB take the wave-per-message index pass
     (index_big_kernel): intact, bit-flipped and truncated ones, mixed with
-    small ones in one batch, against the oracle's verdicts and bytes."""
+    small ones in one batch, against the oracle's verdicts and bytes.  With
+    FSG_DECODE_FORK=1 pass 1b and the large-message exec blocks run on the
+    library's side stream beside the small messages' exec launch (the
+    default for batches of > 128K messages)."""
+    monkeypatch.setenv("FSG_DECODE_FORK", fork)
     rng = np.random.default_rng(21)
     srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (120000, 400000, 1 << 20)]
     srcs.append(fsg.make_batch(fsg.KIND_RANDOM, [70000]).item(0))
@@ -393,12 +398,14 @@ def _copy2(length: int, offset: int) -> bytes:
     return bytes([((length - 1) << 2) | 2]) + offset.to_bytes(2, "little")
 
 
-def test_large_message_segments(gpu, oracle):
+@pytest.mark.parametrize("fork", ["0", "1"])
+def test_large_message_segments(gpu, oracle, fork, monkeypatch):
     """Large bodies run in pass 2 as 64 KiB output segments when no tag spans
     a segment boundary and no copy reaches below its segment (every stream the
     reference encoder writes); otherwise whole.  Raw sizes around the
     boundaries, a tail of < 4 bytes (joins the previous segment), and
-    hand-built streams that must run whole."""
+    hand-built streams that must run whole; on one stream and forked."""
+    monkeypatch.setenv("FSG_DECODE_FORK", fork)
     rng = np.random.default_rng(5)
     items = []
     for n in (65537, 131072, 131073, 131074, 131075, 131076, 196609, 300000, 1 << 20):
