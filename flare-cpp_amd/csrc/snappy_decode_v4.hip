@@ -150,6 +150,102 @@ __device__ __forceinline__ u32 pattern_pieces(u32 len, u32 step) {
 // ===========================================================================
 // Pass 1: index + validate.  One lane per message.
 // ===========================================================================
+// Per-lane start of pass 1 (one message per lane, the whole wave calling):
+// header (ReadUncompressedLength / Parse32WithLimit), slot check, the
+// message's bitmap words (bump-allocated per wave), and the large-message
+// list.  Returns the status (< 0: the lane walk follows) and sets the
+// header length, expected length and bitmap base.
+__device__ __forceinline__ i32 index_prologue(
+    const u8* ib, u32 n_in, bool valid_msg, u32 m, u32 lane, u32 n_msgs, u32 flags,
+    const u32* __restrict__ out_cap, u32* __restrict__ out_len, u32* __restrict__ bm_counter,
+    u32* __restrict__ bm_base_out, u32* __restrict__ bitmap, u64 bm_capacity_words,
+    u32* __restrict__ big_count, u32* __restrict__ big_list, u32 big_threshold, u32* ip,
+    u32* expected, u32* bm_base_ret) {
+  const bool strict = flags & 2u;
+  const bool validate = flags & 1u;
+  i32 status = kOk;  // < 0: parsing
+  if (valid_msg) {
+    u32 ulen = 0;
+    const int h = parse_varint_header(ib, n_in, strict, &ulen);
+    if (h == 0) {
+      status = kBadHeader;
+      out_len[m] = 0;
+    } else {
+      out_len[m] = ulen;
+      *expected = ulen;
+      *ip = (u32)h;
+      status = (!validate && ulen > out_cap[m]) ? kSlotTooSmall : -1;
+    }
+  }
+
+  // ---- bitmap allocation: round_up(ceil(n_in / 32), 4) words, bump-allocated
+  // per wave (order is irrelevant; bases stay 16-byte aligned)
+  u32 bm_base = 0;
+  if (bitmap) {
+    const u32 words = status < 0 ? (((n_in + 31) >> 5) + 3) & ~3u : 0u;
+    const u32 incl = wave_incl_scan(words);
+    const u32 total = readlane(incl, 63);
+    u32 base0 = 0;
+    if (lane == 0 && total) base0 = atomicAdd(bm_counter, total);
+    base0 = readlane(base0, 0);
+    bm_base = base0 + incl - words;
+    if (status < 0 && (u64)bm_base + words > bm_capacity_words) status = kNeedFallback;
+    if (valid_msg) bm_base_out[m] = bm_base;
+  }
+  *bm_base_ret = bm_base;
+
+  // ---- large messages go to index_big_message (a whole wave per message);
+  // one lane would walk them serially for tens of milliseconds
+  if (big_list) {
+    // the largest ones (> kHugeIndexBytes) are listed from the end of the
+    // list so both large-message passes hand them out first
+    const bool big = status < 0 && n_in > big_threshold;
+    const bool huge = big && n_in > kHugeIndexBytes;
+    const u64 bb = __ballot(big && !huge), bh = __ballot(huge);
+    const u64 below = (1ull << lane) - 1;
+    if (bb) {
+      u32 base1 = 0;
+      if (lane == 0) base1 = atomicAdd(big_count, (u32)__builtin_popcountll(bb));
+      base1 = readlane(base1, 0);
+      if (big && !huge) big_list[base1 + (u32)__builtin_popcountll(bb & below)] = m;
+    }
+    if (bh) {
+      u32 base2 = 0;
+      if (lane == 0) base2 = atomicAdd(big_count + 8, (u32)__builtin_popcountll(bh));
+      base2 = readlane(base2, 0);
+      if (huge) big_list[n_msgs - 1 - (base2 + (u32)__builtin_popcountll(bh & below))] = m;
+    }
+    if (big) status = kNeedBigIndex;
+  }
+  return status;
+}
+
+// Pass 1 plan (batches whose large messages are indexed on a side stream):
+// the prologue alone, so pass 1b can start on the listed large messages while
+// the lane walk (index_kernel<true>) runs; lanes left for the walk get
+// kNeedLaneWalk.
+__global__ __launch_bounds__(64) void index_plan_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off,
+    const u32* __restrict__ in_len, u32 n_msgs, const u32* __restrict__ out_cap,
+    u32* __restrict__ out_len, i32* __restrict__ status_out, u32 flags,
+    u32* __restrict__ bm_counter, u32* __restrict__ bm_base_out,
+    u32* __restrict__ bitmap, u64 bm_capacity_words, u32* __restrict__ big_count,
+    u32* __restrict__ big_list, u32 big_threshold) {
+  const u32 lane = threadIdx.x & 63;
+  const u32 m = blockIdx.x * 64 + lane;
+  const bool valid_msg = m < n_msgs;
+  const u8* ib = valid_msg ? in + in_off[m] : in;
+  const u32 n_in = valid_msg ? in_len[m] : 0u;
+  u32 ip = 0, expected = 0, bm_base = 0;
+  const i32 st = index_prologue(ib, n_in, valid_msg, m, lane, n_msgs, flags, out_cap, out_len,
+                                bm_counter, bm_base_out, bitmap, bm_capacity_words, big_count,
+                                big_list, big_threshold, &ip, &expected, &bm_base);
+  if (valid_msg) status_out[m] = st < 0 ? kNeedLaneWalk : st;
+}
+
+// kPlanned: index_plan_kernel ran first (statuses, bitmap bases and the
+// large-message list are in place; only kNeedLaneWalk messages are walked).
+template <bool kPlanned>
 __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, const u32* __restrict__ out_cap,
@@ -190,68 +286,25 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
     tagtab[c] = ((32 - 8 * nb) & 31) | (ll << 5) | (adv << 8) | (len << 16);
   }
   __syncthreads();
-  const bool strict = flags & 2u;
-  const bool validate = flags & 1u;
   const u32 m = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid_msg = m < n_msgs;
 
-  i32 status = kOk;  // < 0: parsing
-  const u8* ib = in;
-  u32 n_in = 0, expected = 0, ip = 0;
-  if (valid_msg) {
-    ib = in + in_off[m];
-    n_in = in_len[m];
+  const u8* ib = valid_msg ? in + in_off[m] : in;
+  const u32 n_in = valid_msg ? in_len[m] : 0u;
+  u32 expected = 0, ip = 0, bm_base = 0;
+  i32 status = kOk;
+  if (!kPlanned) {
+    status = index_prologue(ib, n_in, valid_msg, m, lane, n_msgs, flags, out_cap, out_len,
+                            bm_counter, bm_base_out, bitmap, bm_capacity_words, big_count, big_list,
+                            big_threshold, &ip, &expected, &bm_base);
+  } else if (valid_msg && status_out[m] == kNeedLaneWalk) {
     u32 ulen = 0;
-    const int h = parse_varint_header(ib, n_in, strict, &ulen);
-    if (h == 0) {
-      status = kBadHeader;
-      out_len[m] = 0;
-    } else {
-      out_len[m] = ulen;
-      expected = ulen;
-      ip = (u32)h;
-      status = (!validate && ulen > out_cap[m]) ? kSlotTooSmall : -1;
-    }
+    ip = (u32)parse_varint_header(ib, n_in, flags & 2u, &ulen);  // valid: checked by the plan
+    expected = ulen;
+    bm_base = bitmap ? bm_base_out[m] : 0u;
+    status = -1;
   }
-
-  // ---- bitmap allocation: round_up(ceil(n_in / 32), 4) words, bump-allocated
-  // per wave (order is irrelevant; bases stay 16-byte aligned)
-  u32 bm_base = 0;
-  if (bitmap) {
-    const u32 words = status < 0 ? (((n_in + 31) >> 5) + 3) & ~3u : 0u;
-    const u32 incl = wave_incl_scan(words);
-    const u32 total = readlane(incl, 63);
-    u32 base0 = 0;
-    if (lane == 0 && total) base0 = atomicAdd(bm_counter, total);
-    base0 = readlane(base0, 0);
-    bm_base = base0 + incl - words;
-    if (status < 0 && (u64)bm_base + words > bm_capacity_words) status = kNeedFallback;
-    if (valid_msg) bm_base_out[m] = bm_base;
-  }
-
-  // ---- large messages go to index_big_message (a whole wave per message);
-  // one lane would walk them serially for tens of milliseconds
-  if (big_list) {
-    // the largest ones (> kHugeIndexBytes) are listed from the end of the
-    // list so both large-message passes hand them out first
-    const bool big = status < 0 && n_in > big_threshold;
-    const bool huge = big && n_in > kHugeIndexBytes;
-    const u64 bb = __ballot(big && !huge), bh = __ballot(huge);
-    const u64 below = (1ull << lane) - 1;
-    if (bb) {
-      u32 base1 = 0;
-      if (lane == 0) base1 = atomicAdd(big_count, (u32)__builtin_popcountll(bb));
-      base1 = readlane(base1, 0);
-      if (big && !huge) big_list[base1 + (u32)__builtin_popcountll(bb & below)] = m;
-    }
-    if (bh) {
-      u32 base2 = 0;
-      if (lane == 0) base2 = atomicAdd(big_count + 8, (u32)__builtin_popcountll(bh));
-      base2 = readlane(base2, 0);
-      if (huge) big_list[n_msgs - 1 - (base2 + (u32)__builtin_popcountll(bh & below))] = m;
-    }
-    if (big) status = kNeedBigIndex;
-  }
+  const bool walked = status < 0;  // (planned: the other lanes' statuses stand)
   u32* bm = bitmap ? bitmap + bm_base : nullptr;
 
   const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
@@ -434,8 +487,9 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
     }
     more = __any(status < 0);
   }
-  if (valid_msg) status_out[m] = status;
-  if (valid_msg && bitmap && status == kOk && single_src) bm_base_out[m] = kSingleLiteral | single_src;
+  const bool mine = valid_msg && (!kPlanned || walked);
+  if (mine) status_out[m] = status;
+  if (mine && bitmap && status == kOk && single_src) bm_base_out[m] = kSingleLiteral | single_src;
 }
 
 // ===========================================================================
@@ -1221,15 +1275,24 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   u64 thr = 4 * est_total_in / n_msgs;
   thr = thr < kBigIndexMin ? kBigIndexMin : (thr > kBigIndexMax ? kBigIndexMax : thr);
   const u32 big_threshold = (u32)thr;
-  index_kernel<<<(n_msgs + 64 * kIdxWaves - 1) / (64 * kIdxWaves), 64 * kIdxWaves, 0, stream>>>(
-      in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap, cap_words,
-      big_count, big_list, big_threshold);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  // Pass 1b and the large-message exec blocks run on a side stream, after
-  // pass 1 (which lists the large messages) and beside the one-wave-per-
-  // message exec launch: pass 1b is bound by the serial window walk of the
-  // few largest bodies and leaves most CUs idle, which the small messages'
-  // execution fills.  Both streams join before the fallback pass.
+  const u32 idx_blocks = (n_msgs + 64 * kIdxWaves - 1) / (64 * kIdxWaves);
+  auto launch_index = [&](bool planned) -> hipError_t {
+    if (planned)
+      index_kernel<true><<<idx_blocks, 64 * kIdxWaves, 0, stream>>>(
+          in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
+          cap_words, big_count, big_list, big_threshold);
+    else
+      index_kernel<false><<<idx_blocks, 64 * kIdxWaves, 0, stream>>>(
+          in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
+          cap_words, big_count, big_list, big_threshold);
+    return hipGetLastError();
+  };
+  // Pass 1b and the large-message exec blocks run on a side stream, after a
+  // plan pass (headers, bitmap bases, the large-message list) and beside the
+  // lane walk and the one-wave-per-message exec launch: pass 1b is bound by
+  // the serial window walk of the few largest bodies and leaves most CUs
+  // idle, which the small messages' passes fill.  Both streams join before
+  // the fallback pass.
   // Only for batches of > 128K messages (the mixed-size ones): a fork and
   // join cost ~10 us (C2 0.159 -> 0.169 ms), and uniform batches send nothing
   // to pass 1b (CM 14.4 -> 12.1 ms).  FSG_DECODE_FORK=0/1 forces (A/B).
@@ -1276,16 +1339,25 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   };
   SideStream* side = fork ? side_stream() : nullptr;
   if (side) {
+    // the plan pass lists the large messages; pass 1b starts on them while
+    // the lane walk runs
+    index_plan_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(
+        in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
+        cap_words, big_count, big_list, big_threshold);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     std::lock_guard<std::mutex> lk(side->mu);
     if ((e = hipEventRecord(side->fork, stream)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(side->stream, side->fork, 0)) != hipSuccess) return e;
     if ((e = launch_big(side->stream)) != hipSuccess) return e;
     if ((e = hipEventRecord(side->join, side->stream)) != hipSuccess) return e;
+    if ((e = launch_index(true)) != hipSuccess) return e;
     if ((e = launch_small(stream)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(stream, side->join, 0)) != hipSuccess) return e;
   } else {
-    // one stream: pass 1b, then one exec launch whose first blocks take the
-    // large messages (dispatched first) and the rest one message per wave
+    // one stream: pass 1, pass 1b, then one exec launch whose first blocks
+    // take the large messages (dispatched first) and the rest one message
+    // per wave
+    if ((e = launch_index(false)) != hipSuccess) return e;
     if ((e = launch_index_big(stream)) != hipSuccess) return e;
     exec_kernel<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,

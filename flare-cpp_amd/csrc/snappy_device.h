@@ -35,6 +35,8 @@ constexpr u32 kFlagFallbackOnly = 0x80000000u;
 // Internal: a large message left by the lane-per-message index pass for the
 // wave-per-message one (decode v4), which writes its final status.
 constexpr i32 kNeedBigIndex = 0x20000000;
+// Internal: listed by the decode v4 plan pass for the lane walk.
+constexpr i32 kNeedLaneWalk = 0x10000000;
 
 __host__ __device__ inline u64 max_compressed_length(u64 n) {
   return 32 + n + n / 6;  // snappy.cc:55-77
