@@ -24,6 +24,11 @@ fi
 timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err \
   || { tail -20 $O/bench_default.err; exit 1; }
 cat $O/bench_default.json
+for w in ${BENCH_WORKLOADS:-}; do
+  timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-encode --workload $w \
+    > $O/bench_$w.json 2> $O/bench_$w.err || { tail -20 $O/bench_$w.err; exit 1; }
+  python -c "import json;d=json.load(open('$O/bench_$w.json'));print('$w', d['ms_per_step'], d['value'], d['roofline']['frac'])"
+done
 for WL in c3-decompress cm-decompress; do
   mkdir -p $O/prof_$WL
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$WL -o run -- \
