@@ -18,6 +18,7 @@ bytes) keeps x1.  WRITE_SIZE is exact (C2: 262,144 KB = the output).
 """
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -28,8 +29,8 @@ sys.path.insert(0, str(REPO))
 FETCH_SCALE = {"exec_kernel": 2.0, "index_kernel": 2.0, "index_big_kernel": 2.0}
 
 OP_KERNELS = {
-    "decompress": ("fsg::index_kernel", "fsg::index_big_kernel", "fsg::exec_kernel",
-                   "fsg::decode_pipe_kernel"),
+    "decompress": ("fsg::index_kernel", "fsg::index_plan_kernel", "fsg::index_big_kernel",
+                   "fsg::exec_kernel", "fsg::decode_pipe_kernel"),
     "compress": ("fsg::encode_plan_kernel", "fsg::encode_pipe_kernel", "fsg::encode_gather_kernel"),
 }
 
@@ -39,7 +40,8 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"].split("(")[0]
+        # "void fsg::index_kernel<false>(...)" -> "fsg::index_kernel"
+        name = re.sub(r"<[^>]*>$", "", r["Kernel_Name"].split("(")[0].replace("void ", "", 1))
         vals[name].append(float(r["Counter_Value"]))
     return vals
 
