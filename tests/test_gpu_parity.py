@@ -123,8 +123,12 @@ def test_randomized_against_oracle(gpu, oracle, encoder):
     assert (st == 0).all() and all(o == x for o, x in zip(outs, items))
 
 
-@pytest.mark.parametrize("variant", [0, 3, 4])
-def test_decode_fuzz_against_oracle(gpu, oracle, variant):
+@pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1")])
+def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, monkeypatch):
+    """Mutated and truncated streams (64 B to 70 KB bodies).  fork "1" runs
+    the path of batches over 128K messages: plan pass, side stream, and
+    bodies of <= 1 KiB output decoded one per lane."""
+    monkeypatch.setenv("FSG_DECODE_FORK", fork)
     gpu.codec.select_kernels(variant, 0)
     rng = np.random.default_rng(9)
     srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (64, 700, 9000, 70000)]
