@@ -1,6 +1,6 @@
 #!/bin/bash
 # Builds the GPU codec library of a git revision (default HEAD) into
-# build/ab/lib_prev.so for gpurun_ab.sh's A/B pairs.
+# build/ab/lib_prev.so for tools/gpurun/ab.sh's A/B pairs.
 set -e
 REV=${1:-HEAD}
 D=$(mktemp -d)

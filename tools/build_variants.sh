@@ -1,6 +1,6 @@
 #!/bin/bash
 # Builds build/ab/lib_<name>.so for each "name:FLAGS" argument (the current
-# tree's GPU sources with extra -D flags), for gpurun_abn.sh.
+# tree's GPU sources with extra -D flags), for tools/gpurun/abn.sh.
 set -e
 mkdir -p build/ab
 for spec in "$@"; do

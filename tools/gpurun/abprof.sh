@@ -1,5 +1,5 @@
 #!/bin/bash
-# Kernel-trace stats per A/B library: LIBS="a b" WLS="c3-decompress" bash gpurun_abprof.sh
+# Kernel-trace stats per A/B library: LIBS="a b" WLS="c3-decompress" bash tools/gpurun/abprof.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for w in ${WLS:-c3-decompress}; do
   for n in $LIBS; do

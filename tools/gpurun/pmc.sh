@@ -1,6 +1,6 @@
 #!/bin/bash
 # One PMC pass (SQ counters) over one workload; per-kernel sums printed.
-# usage: WL=cm-decompress bash gpurun_pmc.sh
+# usage: WL=cm-decompress bash tools/gpurun/pmc.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 WL=${WL:-c3-decompress}
 O=gpurun_out/pmc_$WL

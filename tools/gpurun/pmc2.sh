@@ -1,6 +1,6 @@
 #!/bin/bash
 # Two SQ PMC passes (LDS and issue counters) over one workload, each its own run.
-# usage: WL=c3-decompress bash gpurun_pmc2.sh
+# usage: WL=c3-decompress bash tools/gpurun/pmc2.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 WL=${WL:-c3-decompress}
 O=gpurun_out/pmc2_$WL

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel-trace stats for one workload: rocprofv3 --kernel-trace --stats.
-# usage: WL=cm-decompress bash gpurun_prof.sh
+# usage: WL=cm-decompress bash tools/gpurun/prof.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 WL=${WL:-c3-decompress}
 mkdir -p gpurun_out/prof_$WL

@@ -2,7 +2,7 @@
 # Round-2 evidence at HEAD: GPU parity suite, the default bench line, kernel
 # stats for C3 and CM decode, and the FETCH_SIZE / WRITE_SIZE passes for C3
 # decode (each its own rocprofv3 run).  Optional probes first (PROBES=1).
-# usage: bash gpurun_r2.sh   (outputs under gpurun_out/r2/)
+# usage: bash tools/gpurun/r2.sh   (outputs under gpurun_out/r2/)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r2

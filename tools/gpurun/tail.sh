@@ -1,7 +1,7 @@
 #!/bin/bash
 # Launch-order effect: kernel traces of C3 decode steps with and without the
 # trailing fallback launch (FSG_DIAG_NO_TAIL=1); per-kernel start gaps and
-# durations by step.  usage: bash gpurun_tail.sh
+# durations by step.  usage: bash tools/gpurun/tail.sh
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for v in tail notail; do  # FSG_LIB in the environment selects an A/B build
   O=gpurun_out/tail/$v
