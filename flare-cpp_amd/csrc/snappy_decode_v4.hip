@@ -776,7 +776,7 @@ __device__ __forceinline__ void exec_message(
     const u32* __restrict__ in_len, u8* out, const u64* __restrict__ out_off,
     const u32* __restrict__ out_len, i32* __restrict__ status, const u32* __restrict__ bm_base,
     const u32* __restrict__ bitmap, u32* ring, u8* pmap, u8* sb, const u32x4* sel_tab, u32 lane,
-    i32 st, u32 ip0, u32 op0, u32 op1, bool prio) {
+    i32 st, u32 ip0, u32 op0, u32 op1, bool prio, u32 keep_hist) {
   // One message (ip0 = op0 = 0, op1 = its length), or one segment of a large
   // one: output [op0, op1) from the tags starting at input offset ip0, whose
   // copies stay inside the segment (checked by the index walk).
@@ -1011,9 +1011,11 @@ __device__ __forceinline__ void exec_message(
     STAMP(2);
     // ---------- slide the window if this group would overrun it
     if (op + tot_len - sbase > kWindow) {
-      const int nsb = (int)(((op - kKeep + obal) & ~15u)) - (int)obal;
+      const int nsb = (int)(((op - keep_hist + obal) & ~15u)) - (int)obal;
 #if FSG_FLUSH_LAG
-      if ((int)flushed < nsb) {
+      // a far piece (source below the new base) may read up to 15 bytes at
+      // and above the base, so those must be stored too
+      if ((int)flushed < nsb + 16) {
         flush_to((u32)((int)((op + obal) & ~15u) - (int)obal));
         // This group's far loads may read what this flush just stored, with
         // no waited load in between (the ordering argument of DESIGN.md §4
@@ -1138,7 +1140,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     u32* __restrict__ bitmap, const u32* __restrict__ seg_list,
     const u32* __restrict__ seg_count, const u32* __restrict__ whole_list,
     const u32* __restrict__ whole_count, u32* __restrict__ exec_next, u32 big_blocks,
-    u32 big_threshold, u32 prio) {
+    u32 big_threshold, u32 prio, u32 keep_hist) {
   // per wave: the tag ring, then the output window; a large message's index
   // walk stages its input over both (kBigStageBytes + 16 <= their size)
   __shared__ __attribute__((aligned(16))) u8 wl_s[kWavesPerBlock][4 * kTagRing + kWindow + 32];
@@ -1162,7 +1164,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     const u32 m = (blockIdx.x - big_blocks) * kWavesPerBlock + wv;
     if (m < n_msgs && in_len[m] <= big_threshold)
       exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring,
-                   pmap, sb, sel_tab, lane, status[m], 0u, 0u, out_len[m], prio != 0);
+                   pmap, sb, sel_tab, lane, status[m], 0u, 0u, out_len[m], prio != 0, keep_hist);
     return;
   }
   // large messages, listed by pass 1b: whole ones first (the longest start
@@ -1180,7 +1182,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     if (idx < n_whole) {
       const u32 m = whole_list[idx];
       exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring,
-                   pmap, sb, sel_tab, lane, status[m], 0u, 0u, out_len[m], prio != 0);
+                   pmap, sb, sel_tab, lane, status[m], 0u, 0u, out_len[m], prio != 0, keep_hist);
       continue;
     }
     const u64 e = segs[idx - n_whole];
@@ -1193,7 +1195,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     u32 ip0 = 0;  // segment k > 0 starts at the input offset pass 1b left in its slot
     if (k) __builtin_memcpy(&ip0, out + out_off[m] + op0, 4);
     exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, pmap,
-                 sb, sel_tab, lane, status[m], ip0, op0, op1, prio != 0);
+                 sb, sel_tab, lane, status[m], ip0, op0, op1, prio != 0, keep_hist);
   }
 }
 
@@ -1327,6 +1329,14 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     const char* e = getenv("FSG_EXEC_PRIO");
     return e && e[0] == '0' ? 0u : 1u;
   }();
+  // history kept when an exec window slides (FSG_EXEC_KEEP, read per call:
+  // the tests shrink it to exercise the slide's flush rule; 512..3072 bytes,
+  // a multiple of 16)
+  u32 keep_hist = kKeep;
+  if (const char* ke = getenv("FSG_EXEC_KEEP")) {
+    const int v = atoi(ke);
+    if (v >= 512 && v <= 3072 && v % 16 == 0) keep_hist = (u32)v;
+  }
   const char* fork_env = getenv("FSG_DECODE_FORK");  // read per call: tests set it
   const bool fork = fork_env ? atoi(fork_env) != 0 : n_msgs > 131072u;
   const u32 big_blocks = small_blocks < kBigBlocks ? small_blocks : kBigBlocks;
@@ -1349,7 +1359,8 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     exec_kernel<<<big_blocks, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
-        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), big_blocks, big_threshold, 0u);
+        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), big_blocks, big_threshold, 0u,
+        keep_hist);
     return hipGetLastError();
   };
   auto launch_small = [&](hipStream_t st) -> hipError_t {
@@ -1358,7 +1369,8 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     exec_kernel<<<small_blocks, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
-        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), 0u, big_threshold, 0u);
+        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), 0u, big_threshold, 0u,
+        keep_hist);
     return hipGetLastError();
   };
   SideStream* side = fork ? side_stream() : nullptr;
@@ -1387,7 +1399,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
         reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), big_blocks,
-        big_threshold, kPrio);
+        big_threshold, kPrio, keep_hist);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // Diagnostic only (FSG_DIAG_NO_TAIL=1): skip this pass to trace the

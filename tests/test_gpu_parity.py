@@ -494,3 +494,33 @@ def test_mutations_and_trailing_tags(gpu, oracle):
             n_ok += 1
             assert s == fsg.FSG_OK and o[:ulen] == ref, (i, len(c), s)
     assert n_ok > 40 and n_bad > 40
+
+
+@pytest.mark.parametrize("keep", ["512", "768", "1024"])
+def test_window_slide_flush_rule(gpu, oracle, keep, monkeypatch):
+    """A window slide must leave every byte a far piece can read in global
+    memory: the piece's source lies below the new base but its 16-byte load
+    reaches up to 15 bytes above it, so the slide flushes (and waits) when
+    the flush lag leaves fewer than 16 stored bytes at the base.  With the
+    default 2 KiB of kept history that lag is rare; a smaller history
+    (FSG_EXEC_KEEP) makes it frequent.  Before the rule covered the 16
+    bytes, 512 B decoded a zero at offset 343,000 of the 1 MiB golden text.
+    Golden vectors (up to 1 MiB, segmented and whole), window-edge streams
+    and a C3-like batch, byte-equal to the inputs."""
+    monkeypatch.setenv("FSG_EXEC_KEEP", keep)
+    vecs = json.loads((GOLDEN / "vectors.json").read_text())
+    datas = [build_input(v) for v in vecs]
+    comps = [oracle.compress(d) for d in datas]
+    from window_edge import edge_stream
+    rng = np.random.default_rng(41)
+    for _ in range(200):
+        c, raw, _e = edge_stream(rng, int(rng.integers(2000, 40000)))
+        comps.append(c)
+        datas.append(raw)
+    b = fsg.make_batch(fsg.KIND_TEXT, np.full(256, 65536, np.uint32), first_index=777)
+    for i in range(256):
+        datas.append(b.item(i))
+        comps.append(oracle.compress(b.item(i)))
+    outs, ol, st = gpu.decompress(comps, [len(d) for d in datas])
+    for i, (d, o, s) in enumerate(zip(datas, outs, st)):
+        assert s == fsg.FSG_OK and o == d, i
