@@ -995,19 +995,6 @@ __device__ __forceinline__ void exec_message(
       return;
     }
 
-    // ---------- prefetch the next group's tag bytes (lands during this group)
-    {
-      const u32 nh = head + k_tags;
-      const u32 na = tail - nh;
-      const u32 ncnt = na < 64 ? na : 64u;
-      if (lane < ncnt) {
-        const u32 npos = ring[(nh + lane) & (kTagRing - 1)];
-        tv = load16_clamped(ib, npos, n_in, ibal);
-      }
-      pf_head = nh;
-      pf_cnt = ncnt;
-    }
-
     STAMP(2);
     // ---------- slide the window if this group would overrun it
     if (op + tot_len - sbase > kWindow) {
@@ -1015,15 +1002,14 @@ __device__ __forceinline__ void exec_message(
 #if FSG_FLUSH_LAG
       // a far piece (source below the new base) may read up to 15 bytes at
       // and above the base, so those must be stored too
-      if ((int)flushed < nsb + 16) {
-        flush_to((u32)((int)((op + obal) & ~15u) - (int)obal));
-        // This group's far loads may read what this flush just stored, with
-        // no waited load in between (the ordering argument of DESIGN.md §4
-        // needs one): wait until the stores are acknowledged by L2, where
-        // the far loads (sc1) are served.  Rare: only when the flush lag
-        // exceeds the kept history.
-        __builtin_amdgcn_s_waitcnt(0);
-      }
+      if ((int)flushed < nsb + 16) flush_to((u32)((int)((op + obal) & ~15u) - (int)obal));
+      // From this group on, far loads read bytes below the new base + 16:
+      // stored by this flush or by earlier groups' flushes, which may still
+      // be in flight (no waited load was issued after the last of them, the
+      // ordering argument of DESIGN.md §4).  Wait until they are
+      // acknowledged by L2, where the far loads (sc1) are served.  Once per
+      // slide (~every 3 KiB of output).
+      __builtin_amdgcn_s_waitcnt(0);
 #endif
       const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
       for (u32 k = 0; k < keep; k += 1024) {
@@ -1037,6 +1023,20 @@ __device__ __forceinline__ void exec_message(
       sbase = nsb;
       zero_end = (keep + 15) & ~15u;  // the copied blocks end in zeros past op
     }
+    // ---------- prefetch the next group's tag bytes (lands during this group; issued after a
+    // slide's store wait, which then waits only for older operations)
+    {
+      const u32 nh = head + k_tags;
+      const u32 na = tail - nh;
+      const u32 ncnt = na < 64 ? na : 64u;
+      if (lane < ncnt) {
+        const u32 npos = ring[(nh + lane) & (kTagRing - 1)];
+        tv = load16_clamped(ib, npos, n_in, ibal);
+      }
+      pf_head = nh;
+      pf_cnt = ncnt;
+    }
+
     while (op + tot_len + 20 - sbase > zero_end) {  // the group's OR stores land in zeros
       zero_from(zero_end);
       zero_end += 1024;
