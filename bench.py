@@ -91,6 +91,10 @@ def parse(argv=None):
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="weak: every GPU owns a full batch; strong: one batch split by bytes "
                          "(default: per workload, strong for cm/c5)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="decompress on a GPU: time a stream of two alternating batches, batch k+1's "
+                         "tag walk (pass 1, its own stream) beside batch k's execution "
+                         "(fsg_decompress_batch_2s); 0 = one batch, both passes on one stream")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
@@ -204,6 +208,56 @@ def time_steps(torch, device, stream, step, steps, warmup, world, dist):
     return wall / steps, float(np.mean(kern_ms)) / 1e3
 
 
+def time_pipelined(torch, dev, stream, slots, issue, steps, warmup, world, dist):
+    """Times `steps` decodes of a stream of batches: step k decodes slot
+    k % len(slots) with its tag walk on a second stream (`issue(k, s1)`), so
+    batch k+1's walk runs beside batch k's execution.  Step k+len(slots)
+    reuses step k's buffers, so its walk waits for step k's execution (an
+    event): one batch in flight ahead.  Returns (seconds per step, mean
+    per-batch latency in seconds = walk start to execution end)."""
+    s1 = torch.cuda.Stream(dev)
+    nslot = len(slots)
+    done = [None] * nslot
+
+    def run(k, marks=None):
+        sl = k % nslot
+        if done[sl] is not None:
+            s1.wait_event(done[sl])
+        if marks is not None:
+            marks[0][k].record(s1)
+        issue(k, s1)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        done[sl] = ev
+        if marks is not None:
+            marks[1][k].record(stream)
+
+    for k in range(warmup):
+        run(k)
+    _sync(torch, dev)
+    if world > 1:
+        dist.barrier()
+    _sync(torch, dev)
+    done = [None] * nslot
+    t_start = torch.cuda.Event(enable_timing=True)
+    t_end = torch.cuda.Event(enable_timing=True)
+    marks = ([torch.cuda.Event(enable_timing=True) for _ in range(steps)],
+             [torch.cuda.Event(enable_timing=True) for _ in range(steps)])
+    t0 = time.perf_counter()
+    t_start.record(stream)
+    s1.wait_stream(stream)  # the first walk starts after the start mark
+    for k in range(steps):
+        run(k, marks)
+    t_end.record(stream)
+    _sync(torch, dev)
+    if world > 1:
+        dist.barrier()
+    _sync(torch, dev)
+    wall = time.perf_counter() - t0
+    lat = [marks[0][k].elapsed_time(marks[1][k]) for k in range(steps)]
+    return wall / steps, t_start.elapsed_time(t_end) / 1e3 / steps, float(np.mean(lat)) / 1e3
+
+
 def rank_main(args, codec_factory=None):
     """One rank of the benchmark.  `codec_factory(local_rank)` replaces the HIP
     codec only in the CPU launcher test (tests/test_distributed.py)."""
@@ -223,7 +277,8 @@ def rank_main(args, codec_factory=None):
         dist.init_process_group("nccl" if gpu else "gloo", init_method="env://")
         world = dist.get_world_size()
     codec = codec_factory(local) if codec_factory else fsg.SnappyGPU(local)
-    codec.select_kernels(args.decode_kernel, args.encode_kernel)
+    if args.decode_kernel or args.encode_kernel:  # else the library's choice (FSG_DECODE_KERNEL env)
+        codec.select_kernels(args.decode_kernel, args.encode_kernel)
 
     op, kind, n_default, size_spec, scaling_default, desc = WORKLOADS[args.workload]
     scaling = args.scaling or scaling_default
@@ -270,6 +325,7 @@ def rank_main(args, codec_factory=None):
         sample_ok = all(
             host_comp[int(c_off[i]):int(c_off[i]) + int(comp_len[i])].tobytes() == orc.compress(batch.item(int(i)))
             for i in idx)
+        del host_comp
 
     # Decode output slots (exact uncompressed sizes) -- laid out like the raw batch.
     d_out = torch.zeros(max(raw_total, 1), dtype=torch.uint8, device=dev)
@@ -286,14 +342,77 @@ def rank_main(args, codec_factory=None):
 
     step = decode_step if op == "decompress" else encode_step
     algo_bytes = raw_total + comp_total  # each input byte read once, each output byte written once
+
+    # Stream of batches (decompress on a GPU): a second, distinct batch of the
+    # same shape (the next n bodies of the generator), with its own workspace
+    # and outputs; batches alternate.
+    pipe = None
+    if op == "decompress" and gpu and args.pipeline and n:
+        batch2 = fsg.make_batch(kind, batch_sizes(size_spec, first + n, n), first_index=first + n)
+        d_raw2 = H(batch2.data)
+        d_raw2_off, d_raw2_len = H(batch2.offsets), H(batch2.lens)
+        caps2 = np.array([fsg.max_compressed_length(int(x)) for x in batch2.lens], dtype=np.uint64)
+        c2_off, c2_tot = fsg.slot_offsets(caps2)
+        d_comp2 = torch.zeros(c2_tot, dtype=torch.uint8, device=dev)
+        d_comp2_off = H(c2_off)
+        d_comp2_len = torch.zeros(n, dtype=torch.int32, device=dev)
+        d_status2 = torch.zeros(n, dtype=torch.int32, device=dev)
+        max_len2 = int(batch2.lens.max())
+        d_ws2 = codec.compress_workspace(n, max_len2)
+        codec.compress(d_raw2, d_raw2_off, d_raw2_len, n, max_len2, d_comp2, d_comp2_off, d_comp2_len,
+                       d_status2, stream=stream, workspace=d_ws2)
+        del d_ws2
+        _sync(torch, dev)
+        comp_len2 = d_comp2_len.cpu().numpy()[:n].view(np.uint32).copy()
+        errors += int((d_status2 != 0).sum().item())
+        if args.verify_sample > 0:
+            idx = np.linspace(0, n - 1, min(n, args.verify_sample)).astype(np.int64)
+            host_comp2 = d_comp2.cpu().numpy()
+            sample_ok = sample_ok and all(
+                host_comp2[int(c2_off[i]):int(c2_off[i]) + int(comp_len2[i])].tobytes()
+                == orc.compress(batch2.item(int(i))) for i in idx)
+        d_out2 = torch.zeros(max(batch2.total, 1), dtype=torch.uint8, device=dev)
+        d_out_len2 = torch.zeros(n, dtype=torch.int32, device=dev)
+        d_dws2 = codec.decompress_workspace(n, c2_tot)
+        slots = [
+            (d_comp, d_comp_off, d_comp_len, d_out, d_raw_off, d_raw_len, d_out_len, d_status, d_dws),
+            (d_comp2, d_comp2_off, d_comp2_len, d_out2, d_raw2_off, d_raw2_len, d_out_len2, d_status2, d_dws2),
+        ]
+
+        def issue(k, s1):
+            c, co, cl, o, oo, ocap, ol, st, ws = slots[k % 2]
+            codec.decompress(c, co, cl, n, o, oo, ocap, ol, st, stream=stream, workspace=ws, pass1_stream=s1)
+
+        pipe = {"slots": slots, "issue": issue, "raw2": d_raw2, "raw2_total": batch2.total,
+                "comp2_total": int(comp_len2.astype(np.uint64).sum())}
     gen_s = time.time() - t_gen
 
-    t_step, avg_kernel_s = time_steps(torch, dev, stream, step, args.steps, args.warmup, world, dist)
+    pipeline_info = None
+    if pipe is not None:
+        t_step, avg_kernel_s, lat_s = time_pipelined(torch, dev, stream, pipe["slots"], pipe["issue"],
+                                                     args.steps, args.warmup, world, dist)
+        # the same batch, both passes on one stream, for comparison (untimed in `value`)
+        t_serial, k_serial = time_steps(torch, dev, stream, step, args.steps, 1, world, dist)
+        # both batches' bytes per step pair: the mean over the stream
+        algo_bytes = (raw_total + comp_total + pipe["raw2_total"] + pipe["comp2_total"]) / 2
+        pipeline_info = {
+            "batches": 2,
+            "mode": "batch k+1's tag walk (pass 1) on a second stream beside batch k's execution "
+                    "(fsg_decompress_batch_2s); one batch in flight ahead",
+            "latency_ms_per_batch": round(lat_s * 1e3, 4),
+            "serial_ms_per_step": round(k_serial * 1e3, 4),
+        }
+    else:
+        t_step, avg_kernel_s = time_steps(torch, dev, stream, step, args.steps, args.warmup, world, dist)
 
     # Correctness of the timed output (device-side, untimed).
     errors += int((d_status[:n] != 0).sum().item())
     if op == "decompress":
         roundtrip_ok = bool(torch.equal(d_out[:raw_total], d_raw[:raw_total]))
+        if pipe is not None:
+            _, _, _, o2, _, _, _, st2, _ = pipe["slots"][1]
+            errors += int((st2 != 0).sum().item())
+            roundtrip_ok = roundtrip_ok and bool(torch.equal(o2[:pipe["raw2_total"]], pipe["raw2"]))
     else:
         roundtrip_ok = bool((d_comp_len.cpu().numpy()[:n].view(np.uint32) == comp_len).all())
 
@@ -308,12 +427,17 @@ def rank_main(args, codec_factory=None):
         rscatter = root_scatter(torch, dist, dev, stream, world, rank, codec, d_comp, d_comp_off,
                                 d_comp_len, n, d_raw, d_raw_len, d_raw_off, raw_total, c_tot)
 
+    # bytes per step: a pipelined run alternates two batches (their mean)
+    raw_v, comp_v = raw_total, comp_total
+    if pipe is not None:
+        raw_v = (raw_total + pipe["raw2_total"]) // 2
+        comp_v = (comp_total + pipe["comp2_total"]) // 2
     if world > 1:
         t_step, avg_kernel_s, (raw_all, comp_all, errors, bad) = shard.reduce_measurements(
-            dist, dev, t_step, avg_kernel_s, raw_total, comp_total, errors, int(not roundtrip_ok))
+            dist, dev, t_step, avg_kernel_s, raw_v, comp_v, errors, int(not roundtrip_ok))
         roundtrip_ok = bad == 0
     else:
-        raw_all, comp_all = raw_total, comp_total
+        raw_all, comp_all = raw_v, comp_v
 
     # The encode leg of the default decode run (same bodies, already resident).
     enc = None
@@ -372,16 +496,19 @@ def rank_main(args, codec_factory=None):
                 "traffic": pmc.get("traffic_bytes_per_launch") if pmc else None,
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "avg_kernel_ms": round(avg_kernel_s * 1e3, 4),
-                "read_frac": round((comp_total if op == "decompress" else raw_total) / avg_kernel_s / 1e9
+                "read_frac": round((comp_v if op == "decompress" else raw_v) / avg_kernel_s / 1e9
                                    / HBM_PEAK_GBS, 4),
-                "note": "rank 0's bytes / MAX over ranks of the HIP-event launch time" if world > 1 else
-                        "algorithmic bytes / average HIP-event duration of one launch on its stream",
+                "note": ("rank 0's bytes / MAX over ranks of the HIP-event launch time" if world > 1 else
+                         "algorithmic bytes / average HIP-event duration of one launch on its stream")
+                        + ("; pipelined: HIP-event time of the whole stream of batches / steps"
+                           if pipeline_info else ""),
             },
             "cpu_baseline": cpu,
             "encode": enc,
             "end_to_end": e2e,
             "multi_gpu": {"allgather": gather, "root_scatter": rscatter} if world > 1 else None,
             "correct": {"status_errors": errors, "roundtrip_ok": roundtrip_ok, "oracle_sample_ok": sample_ok},
+            "pipeline": pipeline_info,
             "kernel_src": kernel_source_hash(),
             "kernels": {"decode": args.decode_kernel, "encode": args.encode_kernel},
             "setup_s": round(gen_s, 2),

@@ -23,7 +23,8 @@ size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes);
 hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u8* out, const u64* out_off,
                             const u32* out_cap, u32* out_len, i32* status,
-                            u32 flags, void* ws, size_t ws_bytes, hipStream_t stream);
+                            u32 flags, void* ws, size_t ws_bytes, hipStream_t stream,
+                            int exec_variant, hipStream_t pass1_stream);
 hipError_t launch_headers(const u8* in, const u64* in_off, const u32* in_len,
                           u32 n_msgs, u32* ulen, int lenient, hipStream_t stream);
 size_t encode_tables_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out);
@@ -82,7 +83,7 @@ int fsg_set_split_region_cap(uint32_t bytes) {
 int fsg_select_kernels(int decode_variant, int encode_variant) {
   // generation 2 (persistent-lane decode, literal lane encode) was retired:
   // superseded by 3/4 on every workload
-  if (decode_variant < 0 || decode_variant > 4 || decode_variant == 2 || encode_variant < 0 ||
+  if (decode_variant < 0 || decode_variant > 5 || decode_variant == 2 || encode_variant < 0 ||
       encode_variant > 3 || encode_variant == 2)
     return FSG_ERR_INVALID_ARG;
   g_decode_variant.store(decode_variant);
@@ -182,12 +183,42 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
                 "fsg_compress_batch");
 }
 
+namespace {
+int decompress_impl(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                    uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off,
+                    const uint32_t* d_out_cap, uint32_t* d_out_len, int32_t* d_status,
+                    uint32_t flags, void* d_workspace, size_t workspace_bytes, void* stream,
+                    void* pass1_stream);
+}  // namespace
+
 int fsg_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
                          const uint32_t* d_in_len, uint32_t n_msgs,
                          uint8_t* d_out, const uint64_t* d_out_off,
                          const uint32_t* d_out_cap, uint32_t* d_out_len,
                          int32_t* d_status, uint32_t flags, void* d_workspace,
                          size_t workspace_bytes, void* stream) {
+  return decompress_impl(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                         d_status, flags, d_workspace, workspace_bytes, stream, nullptr);
+}
+
+int fsg_decompress_batch_2s(const uint8_t* d_in, const uint64_t* d_in_off,
+                            const uint32_t* d_in_len, uint32_t n_msgs,
+                            uint8_t* d_out, const uint64_t* d_out_off,
+                            const uint32_t* d_out_cap, uint32_t* d_out_len,
+                            int32_t* d_status, uint32_t flags, void* d_workspace,
+                            size_t workspace_bytes, void* stream, void* pass1_stream) {
+  return decompress_impl(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                         d_status, flags, d_workspace, workspace_bytes, stream, pass1_stream);
+}
+
+}  // extern "C"
+
+namespace {
+int decompress_impl(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                    uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off,
+                    const uint32_t* d_out_cap, uint32_t* d_out_len, int32_t* d_status,
+                    uint32_t flags, void* d_workspace, size_t workspace_bytes, void* stream,
+                    void* pass1_stream) {
   const bool validate = flags & FSG_FLAG_VALIDATE_ONLY;
   if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out_len || !d_status ||
                  (!validate && (!d_out || !d_out_off || !d_out_cap))))
@@ -198,24 +229,40 @@ int fsg_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
   // tags without touching output for validate-only.  FSG_DECODE_KERNEL or
   // fsg_select_kernels force a variant (A/B runs).
   const int forced = g_decode_variant.load(std::memory_order_relaxed);
+  const bool v4_fits = d_workspace && workspace_bytes >= fsg::decode_v4_workspace_bytes(n_msgs, 0);
+  const bool two_pass = !validate && forced != 1 && forced != 3 && v4_fits;
+  if (!two_pass && pass1_stream && pass1_stream != stream) {
+    // single-pass kernels run on `stream` alone: order it after pass1_stream,
+    // where the caller made the inputs ready
+    hipEvent_t ev = nullptr;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev, (hipStream_t)pass1_stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent((hipStream_t)stream, ev, 0);
+    if (ev) (void)hipEventDestroy(ev);
+    if (e != hipSuccess) return record(e, "fsg_decompress_batch_2s");
+  }
   if (validate || forced == 1)
     return record(fsg::launch_decode(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
                                      d_out_cap, d_out_len, d_status, flags,
                                      (hipStream_t)stream),
                   "fsg_decompress_batch");
-  const bool v4_fits = d_workspace && workspace_bytes >= fsg::decode_v4_workspace_bytes(n_msgs, 0);
-  if ((forced == 0 || forced == 4) && v4_fits) {
+  if (two_pass) {
     // (messages whose bitmap does not fit the workspace are finished by the
-    // v4 launches' serial fallback pass)
+    // two-pass launches' serial fallback pass).  Execution pass: one tag per
+    // lane (5, the default) or <= 16-byte pieces per lane (4).
     return record(fsg::launch_decode_v4(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
                                         d_out_cap, d_out_len, d_status, flags, d_workspace,
-                                        workspace_bytes, (hipStream_t)stream),
+                                        workspace_bytes, (hipStream_t)stream, forced == 4 ? 4 : 5,
+                                        (hipStream_t)pass1_stream),
                   "fsg_decompress_batch");
   }
   return record(fsg::launch_decode_v3(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off,
                                       d_out_cap, d_out_len, d_status, flags, (hipStream_t)stream),
                 "fsg_decompress_batch");
 }
+}  // namespace
+
+extern "C" {
 
 // ---- LZ4 (include/flare_lz4_gpu.h)
 size_t fsg_lz4_max_compressed_length(size_t n) { return 5 + n + n / 255 + 16; }

@@ -116,13 +116,65 @@ __device__ __forceinline__ void wave_lds_fence() { __builtin_amdgcn_wave_barrier
 
 // 16 bytes of a message buffer at `off`, never touching bytes outside
 // [-(bal), limit) (see clamped_origin).
-__device__ __forceinline__ u32x4 load16_clamped(const u8* base, u32 off, u32 limit, u32 bal) {
+[[maybe_unused]] __device__ __forceinline__ u32x4 load16_clamped(const u8* base, u32 off, u32 limit, u32 bal) {
   const int a = clamped_origin(off, limit, bal);
   u32x4 v;
   __builtin_memcpy(&v, base + a, 16);
   const u32 sh = (u32)((int)off - a);
   return sh ? shr_bytes(v, sh) : v;
 }
+
+// A message's compressed bytes as a buffer: base = the 16-byte-aligned block
+// holding its first byte, num_records = its last byte's dword end.  A raw
+// buffer load returns 0 for every dword that reaches past num_records and
+// touches no memory there (per dword, measured on gfx950:
+// tools/probes/buffer_oob_probe.hip), so loads at dword-aligned offsets need
+// no clamping: every dword holding a message byte lies inside the aligned
+// block structure the message occupies.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t msg_rsrc(const u8* abase, u32 bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<u8*>(abase), (short)0,
+                                           (int)((bytes + 3) & ~3u), 0x00020000);
+}
+
+// 16 bytes at buffer offset P (any alignment): one 16-byte and one 4-byte
+// load at the dword below P, then a byte shift (bytes past the end read 0).
+__device__ __forceinline__ u32x4 rsrc_load16(__amdgpu_buffer_rsrc_t r, u32 P) {
+  const u32 a = P & ~3u, s = P & 3u;
+  const u32x4 d = __builtin_amdgcn_raw_buffer_load_b128(r, a, 0, 0);
+  const u32 d4 = __builtin_amdgcn_raw_buffer_load_b32(r, a + 16, 0, 0);
+  return u32x4{__builtin_amdgcn_alignbyte(d[1], d[0], s), __builtin_amdgcn_alignbyte(d[2], d[1], s),
+               __builtin_amdgcn_alignbyte(d[3], d[2], s), __builtin_amdgcn_alignbyte(d4, d[3], s)};
+}
+
+// The same in two steps, so that several loads are in flight before the
+// first shift waits for its data: raw_load16 issues the loads, shifted16
+// applies the byte shift.
+struct Raw16 {
+  u32x4 d;
+  u32 d4, s;
+};
+__device__ __forceinline__ Raw16 raw_load16(__amdgpu_buffer_rsrc_t r, u32 P) {
+  const u32 a = P & ~3u;
+  return Raw16{__builtin_amdgcn_raw_buffer_load_b128(r, a, 0, 0),
+               __builtin_amdgcn_raw_buffer_load_b32(r, a + 16, 0, 0), P & 3u};
+}
+__device__ __forceinline__ u32x4 shifted16(const Raw16& x) {
+  return u32x4{__builtin_amdgcn_alignbyte(x.d[1], x.d[0], x.s), __builtin_amdgcn_alignbyte(x.d[2], x.d[1], x.s),
+               __builtin_amdgcn_alignbyte(x.d[3], x.d[2], x.s), __builtin_amdgcn_alignbyte(x.d4, x.d[3], x.s)};
+}
+
+// The 5 tag bytes at buffer offset P: bytes P..P+3 in .x, byte P+4 in the low
+// byte of .y (one 8-byte load at the dword below P).
+__device__ __forceinline__ u32x2 rsrc_tag5(__amdgpu_buffer_rsrc_t r, u32 P) {
+  const u32 a = P & ~3u, s = P & 3u;
+  const u32x2 d = __builtin_amdgcn_raw_buffer_load_b64(r, a, 0, 0);
+  return u32x2{__builtin_amdgcn_alignbyte(d[1], d[0], s), d[1] >> (8 * s)};
+}
+
+// Waits for every outstanding memory operation of the wave.  The asm
+// statement clobbers memory, so the compiler keeps later loads after it
+// (the bare s_waitcnt builtin is not a memory barrier to the optimizer).
+__device__ __forceinline__ void wait_all_memory() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
 
 // Inclusive prefix sum over the 64 lanes with DPP row shifts and row
 // broadcasts (gfx9 wave64): 7 VALU steps, no LDS round trip.
@@ -721,6 +773,11 @@ namespace {
 #endif
 constexpr u32 kWindow = FSG_WINDOW;  // LDS output window per wave
 constexpr u32 kKeep = FSG_KEEP;      // history kept when the window slides
+// After a slide op - sbase <= keep + 15; a group adds <= 16 * kMaxPieces
+// bytes and an OR store writes up to 20 bytes past a piece's start, all of
+// which must stay inside the window's kWindow + 32 bytes.
+constexpr u32 kMaxKeep = (kWindow - 16 * 64 - 48) & ~15u;
+static_assert(kKeep <= kMaxKeep, "kept history leaves room for one group");
 
 __device__ __forceinline__ u32x4 lds_read16(const u8* p) {
   u32x4 v;
@@ -731,25 +788,39 @@ __device__ __forceinline__ u32x4 lds_read16(const u8* p) {
 // OR n (1..16) bytes of v into the window at byte offset w, whose bytes
 // there are zero: five aligned ds_or_b32 whatever w and n, so the LDS time
 // is fixed per instruction instead of per misaligned lane, and no size
-// branches.  Bytes past n are masked to zero, so nothing lands past w + n.
-__device__ __forceinline__ void or_store(u8* sb, u32 w, u32x4 v, u32 n) {
-#pragma unroll
-  for (u32 k = 0; k < 4; ++k) {
-    const u32 have = n > 4 * k ? n - 4 * k : 0u;
-    v[k] &= have >= 4 ? 0xffffffffu : (have ? 0xffffffffu >> (32 - 8 * have) : 0u);
-  }
-  const u32 b = w & 3;
-  const u32 o0 = v[0] << (8 * b);
-  const u32 o1 = b ? alignbyte(v[1], v[0], 4 - b) : v[1];
-  const u32 o2 = b ? alignbyte(v[2], v[1], 4 - b) : v[2];
-  const u32 o3 = b ? alignbyte(v[3], v[2], 4 - b) : v[3];
-  const u32 o4 = b ? v[3] >> (32 - 8 * b) : 0u;
+// branches.  Bytes past n are masked to zero (mtab[n]: the byte mask of n
+// bytes, a 17-entry LDS table), so nothing lands past w + n; the shift by
+// w & 3 bytes is one v_perm per output dword (selector byte j = 4 + j - b
+// picks byte j - b of the pair (v[k], v[k-1])).  10 VALU, where computing
+// the masks and shifts inline took ~40.
+__device__ __forceinline__ void or_store(u8* sb, u32 w, u32x4 v, u32 n, const u32x4* mtab) {
+  const u32x4 mk = mtab[n];
+  v[0] &= mk[0];
+  v[1] &= mk[1];
+  v[2] &= mk[2];
+  v[3] &= mk[3];
+  // bytes 4-b .. 7-b: the 8-byte sequence 01..08 from byte 3-b = (~w) & 3
+  const u32 sel = __builtin_amdgcn_alignbyte(0x08070605u, 0x04030201u, ~w);
+  const u32 o0 = __builtin_amdgcn_perm(v[0], 0u, sel);
+  const u32 o1 = __builtin_amdgcn_perm(v[1], v[0], sel);
+  const u32 o2 = __builtin_amdgcn_perm(v[2], v[1], sel);
+  const u32 o3 = __builtin_amdgcn_perm(v[3], v[2], sel);
+  const u32 o4 = __builtin_amdgcn_perm(0u, v[3], sel);
   u32* d = reinterpret_cast<u32*>(sb) + (w >> 2);
   __hip_atomic_fetch_or(d + 0, o0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __hip_atomic_fetch_or(d + 1, o1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __hip_atomic_fetch_or(d + 2, o2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __hip_atomic_fetch_or(d + 3, o3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __hip_atomic_fetch_or(d + 4, o4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// mtab[n] (n = 0..16): 0xff in the first n bytes.  68 threads fill it.
+__device__ __forceinline__ void init_mask_table(u32x4* mtab, u32 t) {
+  if (t < 68) {
+    const u32 n = t >> 2, q = t & 3;
+    const u32 have = n > 4 * q ? n - 4 * q : 0u;
+    reinterpret_cast<u32*>(mtab)[t] = have >= 4 ? 0xffffffffu : (have ? 0xffffffffu >> (32 - 8 * have) : 0u);
+  }
 }
 
 }  // namespace
@@ -775,8 +846,8 @@ __device__ __forceinline__ void exec_message(
     u32 m, const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u8* out, const u64* __restrict__ out_off,
     const u32* __restrict__ out_len, i32* __restrict__ status, const u32* __restrict__ bm_base,
-    const u32* __restrict__ bitmap, u32* ring, u8* pmap, u8* sb, const u32x4* sel_tab, u32 lane,
-    i32 st, u32 ip0, u32 op0, u32 op1, bool prio, u32 keep_hist) {
+    const u32* __restrict__ bitmap, u32* ring, u8* pmap, u8* sb, const u32x4* sel_tab,
+    const u32x4* mtab, u32 lane, i32 st, u32 ip0, u32 op0, u32 op1, bool prio, u32 keep_hist) {
   // One message (ip0 = op0 = 0, op1 = its length), or one segment of a large
   // one: output [op0, op1) from the tags starting at input offset ip0, whose
   // copies stay inside the segment (checked by the index walk).
@@ -789,6 +860,8 @@ __device__ __forceinline__ void exec_message(
   if (st != kOk) return;
   const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
   const u32 obal = (u32)(reinterpret_cast<uintptr_t>(ob) & 15);
+  // the message's input as a buffer: tag and literal loads need no clamping
+  const __amdgpu_buffer_rsrc_t irsrc = msg_rsrc(ib - ibal, ibal + n_in);
 #if FSG_FAR_SC1
   // the message's slot as a buffer: far copies load through it past L1
   const __amdgpu_buffer_rsrc_t orsrc =
@@ -804,7 +877,7 @@ __device__ __forceinline__ void exec_message(
 #pragma unroll
       for (u32 r = 0; r < 4; ++r) {
         const u32 k = k0 + 1024 * r + lane * 16;
-        x[r] = k < expected ? load16_clamped(ib, S + k, n_in, ibal) : u32x4{0, 0, 0, 0};
+        x[r] = k < expected ? rsrc_load16(irsrc, S + k + ibal) : u32x4{0, 0, 0, 0};
       }
 #pragma unroll
       for (u32 r = 0; r < 4; ++r) {
@@ -840,7 +913,7 @@ __device__ __forceinline__ void exec_message(
   };
   u32 bmw = fill_word(scan);
   u32 pf_head = 0xffffffffu, pf_cnt = 0;  // tag bytes prefetched for ring [pf_head, +pf_cnt)
-  u32x4 tv = u32x4{0, 0, 0, 0};
+  u32x2 tv = u32x2{0, 0};
 
   // Store window bytes [flushed, fe) to the slot: one 16-byte block per lane,
   // whole aligned blocks with one store, partial edge blocks exactly.
@@ -889,7 +962,7 @@ __device__ __forceinline__ void exec_message(
     const bool valid = lane < take0;
     const u32 pos = valid ? ring[(head + lane) & (kTagRing - 1)] : 0u;
     if (pf_head != head || pf_cnt < take0)
-      tv = valid ? load16_clamped(ib, pos, n_in, ibal) : u32x4{0, 0, 0, 0};
+      tv = valid ? rsrc_tag5(irsrc, pos + ibal) : u32x2{0, 0};
 
     // ---------- decode one tag per lane (checked by pass 1)
     // A wave on its way to the group's global loads (round A; and the bitmap
@@ -933,7 +1006,7 @@ __device__ __forceinline__ void exec_message(
 #pragma unroll
         for (u32 r = 0; r < 4; ++r) {
           const u32 k = k0 + 1024 * r + lane * 16;
-          x[r] = k < L ? load16_clamped(ib, S + k, n_in, ibal) : u32x4{0, 0, 0, 0};
+          x[r] = k < L ? rsrc_load16(irsrc, S + k + ibal) : u32x4{0, 0, 0, 0};
         }
 #pragma unroll
         for (u32 r = 0; r < 4; ++r) {
@@ -954,7 +1027,7 @@ __device__ __forceinline__ void exec_message(
         const u32 lo = (u32)sbase + 16 * lane;
         if (lo < op) {
           const u32 cnt = op - lo < 16 ? op - lo : 16u;
-          store_exact(sb + 16 * lane, load16_clamped(ib, S + L - (op - lo), n_in, ibal), cnt);
+          store_exact(sb + 16 * lane, rsrc_load16(irsrc, S + L - (op - lo) + ibal), cnt);
         }
       }
       wave_lds_fence();
@@ -1009,7 +1082,7 @@ __device__ __forceinline__ void exec_message(
       // ordering argument of DESIGN.md §4).  Wait until they are
       // acknowledged by L2, where the far loads (sc1) are served.  Once per
       // slide (~every 3 KiB of output).
-      __builtin_amdgcn_s_waitcnt(0);
+      wait_all_memory();
 #endif
       const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
       for (u32 k = 0; k < keep; k += 1024) {
@@ -1031,7 +1104,7 @@ __device__ __forceinline__ void exec_message(
       const u32 ncnt = na < 64 ? na : 64u;
       if (lane < ncnt) {
         const u32 npos = ring[(nh + lane) & (kTagRing - 1)];
-        tv = load16_clamped(ib, npos, n_in, ibal);
+        tv = rsrc_tag5(irsrc, npos + ibal);
       }
       pf_head = nh;
       pf_cnt = ncnt;
@@ -1068,9 +1141,9 @@ __device__ __forceinline__ void exec_message(
     u32x4 xa = u32x4{0, 0, 0, 0};
     if (global_src)
 #if FSG_FAR_SC1
-      xa = kT == 0 ? load16_clamped(ib, src, n_in, ibal) : far_load(orsrc, src + obal);
+      xa = kT == 0 ? rsrc_load16(irsrc, src + ibal) : far_load(orsrc, src + obal);
 #else
-      xa = kT == 0 ? load16_clamped(ib, src, n_in, ibal) : load16_clamped(ob, src, expected, obal);
+      xa = kT == 0 ? rsrc_load16(irsrc, src + ibal) : load16_clamped(ob, src, expected, obal);
 #endif
     if (prio) __builtin_amdgcn_s_setprio(0);
     // the previous group's completed blocks are flushed while these loads are
@@ -1105,7 +1178,7 @@ __device__ __forceinline__ void exec_message(
       if (ready) {
         u32x4 x = lds_read16(sb + ((int)src - sbase));
         if (kT == 2) x = expand_pattern(x, offT, sel_tab);
-        or_store(sb, (u32)((int)dst - sbase), x, n);
+        or_store(sb, (u32)((int)dst - sbase), x, n, mtab);
       }
       wave_lds_fence();
       pend &= ~__ballot(ready);
@@ -1126,12 +1199,372 @@ __device__ __forceinline__ void exec_message(
 #endif
 }
 
+// ===========================================================================
+// Pass 2, v5 (default): one TAG per lane.
+//
+// Same walk as v4 (tag ring from the bitmap, LDS output window, far copies
+// from the slot, flush, slide, long literals), with the per-group work cut
+// down to what a tag needs:
+//   - the next group's tag bytes are prefetched as 20 bytes per lane (one
+//     16-byte and one 4-byte buffer load at the dword below the tag: no
+//     clamping, bytes past the message read 0), so a short literal's bytes
+//     (<= 16 of them follow the tag byte) are already in registers -- a
+//     literal tag needs no load of its own;
+//   - the tag is decoded through a 256-entry table in LDS (char_table,
+//     snappy.cc:516-549);
+//   - no piece map: a lane executes its own tag as <= 4 chunks of 16 bytes.
+//     Round A writes every chunk whose source is in registers or global
+//     memory (literals, far copies); rounds B run the near chunks in
+//     dependency order (a chunk runs once its source ends at or below the
+//     first unfinished chunk of the group).  A copy with offset < 16 that
+//     overlaps itself writes pat_step(off)-byte chunks of its expanded
+//     pattern; each later chunk copies the previous one.
+// ===========================================================================
+namespace {
+constexpr u32 kGroupBytes = 1024;  // output bytes per group (as v4: 64 pieces x 16)
+
+// Per tag byte c: bits 0-4 the right shift of 0xffffffff that masks the nb
+// extra bytes ((32 - 8 nb) & 31), bit 5 long literal (length = extra + 1),
+// bit 6 literal, bits 8-14 length (short literal, copies), bits 16-18 nb,
+// bits 20-30 COPY_1's offset bits 8-10 (snappy.cc:744-781).
+__device__ __forceinline__ u32 exec_tag_entry(u32 c) {
+  const u32 type = c & 3, l0 = (c >> 2) + 1;
+  u32 nb, len, lit = 0, ll = 0, hi = 0;
+  if (type == 0) {
+    lit = 1;
+    nb = l0 > 60 ? l0 - 60 : 0;
+    ll = nb ? 1 : 0;
+    len = nb ? 0 : l0;
+  } else if (type == 1) {
+    nb = 1;
+    len = 4 + ((c >> 2) & 7);
+    hi = (c >> 5) << 8;
+  } else {
+    nb = type == 2 ? 2 : 4;
+    len = l0;
+  }
+  return ((32 - 8 * nb) & 31) | (ll << 5) | (lit << 6) | (len << 8) | (nb << 16) | (hi << 20);
+}
+}  // namespace
+
+__device__ __forceinline__ void exec5_message(
+    u32 m, const u8* __restrict__ in, const u64* __restrict__ in_off,
+    const u32* __restrict__ in_len, u8* out, const u64* __restrict__ out_off,
+    const u32* __restrict__ out_len, i32* __restrict__ status, const u32* __restrict__ bm_base,
+    const u32* __restrict__ bitmap, u32* ring, const u32* tagtab, u8* sb, const u32x4* sel_tab,
+    const u32x4* mtab, u32 lane, i32 st, u32 ip0, u32 op0, u32 op1, bool prio, u32 keep_hist) {
+  const u32 bmb = bm_base[m];
+  const u32 n_in = in_len[m];
+  const u32 expected = out_len[m];
+  const u8* ib = in + in_off[m];
+  u8* ob = out + out_off[m];
+  if (st != kOk) return;
+  const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
+  const u32 obal = (u32)(reinterpret_cast<uintptr_t>(ob) & 15);
+  const __amdgpu_buffer_rsrc_t irsrc = msg_rsrc(ib - ibal, ibal + n_in);
+  // the slot as a buffer: far copies load through it past L1 (see far_load)
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc(ob - obal, (short)0, (int)(expected + obal), 0x00020000);
+
+  if ((bmb & kSingleLiteral) && op1 == expected && op0 == 0) {
+    const u32 S = bmb & ~kSingleLiteral;
+    for (u32 k0 = 0; k0 < expected; k0 += 4096) {
+      Raw16 x[4];
+#pragma unroll
+      for (u32 r = 0; r < 4; ++r) x[r] = raw_load16(irsrc, S + k0 + 1024 * r + lane * 16 + ibal);
+#pragma unroll
+      for (u32 r = 0; r < 4; ++r) {
+        const u32 k = k0 + 1024 * r + lane * 16;
+        if (k < expected) store_exact(ob + k, shifted16(x[r]), expected - k < 16 ? expected - k : 16u);
+      }
+    }
+    return;
+  }
+  const u32* bm = bitmap + bmb;
+  const u32 nwords = (n_in + 31) >> 5;
+
+  u32 head = 0, tail = 0, scan = ip0 >> 5, op = op0;
+  int sbase = (int)((op0 + obal) & ~15u) - (int)obal;  // output position of sb[0]
+  u32 flushed = op0;                                    // output [op0, flushed) is in global memory
+  auto zero_from = [&](u32 from) {  // 1 KiB of zeros at a 16-aligned offset
+    const u32 i = from + 16 * lane;
+    if (i < kWindow + 32) *reinterpret_cast<u32x4*>(sb + i) = u32x4{0, 0, 0, 0};
+  };
+  zero_from(0);
+  u32 zero_end = 1024;
+  wave_lds_fence();
+  auto fill_word = [&](u32 sc) -> u32 {
+    const u32 wi = sc + (lane >> 2);
+    return (lane < 4 * kFillWords && wi < nwords) ? bm[wi] : 0u;
+  };
+  u32 bmw = fill_word(scan);
+  // the next group's tag bytes: 20 bytes from the dword below the tag
+  u32 pf_head = 0xffffffffu, pf_cnt = 0;
+  u32x4 pd = u32x4{0, 0, 0, 0};
+  u32 pd4 = 0;
+  auto prefetch = [&](u32 p) {
+    const u32 a = (p + ibal) & ~3u;
+    pd = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
+    pd4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
+  };
+
+  auto flush_to = [&](u32 fe) {
+    if (fe <= flushed) return;
+    const int b0 = (int)(((flushed + obal) & ~15u)) - (int)obal;
+    for (int blk = b0 + 16 * (int)lane; blk < (int)fe; blk += 1024) {
+      const u32 lo = blk < (int)flushed ? flushed : (u32)blk;
+      const u32 hi = blk + 16 < (int)fe ? (u32)(blk + 16) : fe;
+      if (hi - lo == 16) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(sb + (blk - sbase));
+        __builtin_memcpy(ob + blk, &v, 16);
+      } else {
+        store_exact(ob + lo, lds_read16(sb + ((int)lo - sbase)), hi - lo);
+      }
+    }
+    flushed = fe;
+  };
+
+  for (;;) {
+    // ---------- refill the tag ring from the bitmap (as v4)
+    if (tail - head < 2 * kMaxPieces && scan < nwords) {
+      if (prio) __builtin_amdgcn_s_setprio(1);
+      u32 bits = (bmw >> (8 * (lane & 3))) & 0xffu;
+      const u32 bitbase = (scan + (lane >> 2)) * 32 + 8 * (lane & 3);
+      if (bitbase < ip0) bits &= bitbase + 8 <= ip0 ? 0u : (0xffu << (ip0 - bitbase)) & 0xffu;
+      const u32 cnt = __builtin_popcount(bits);
+      const u32 incl = dpp_incl_scan(cnt);
+      u32 slot = tail + incl - cnt;
+      while (bits) {
+        ring[slot & (kTagRing - 1)] = bitbase + __builtin_ctz(bits);
+        ++slot;
+        bits &= bits - 1;
+      }
+      tail += readlane(incl, 63);
+      scan += kFillWords;
+      bmw = fill_word(scan);
+      wave_lds_fence();
+      continue;
+    }
+    const u32 avail = tail - head;
+    if (avail == 0 || op >= op1) break;
+    const u32 take0 = avail < 64 ? avail : 64u;
+    const bool valid = lane < take0;
+    const u32 pos = valid ? ring[(head + lane) & (kTagRing - 1)] : 0u;
+    if (pf_head != head || pf_cnt < take0) {
+      if (valid) prefetch(pos);
+    }
+    if (prio) __builtin_amdgcn_s_setprio(1);
+
+    // ---------- decode one tag per lane (checked by pass 1)
+    const u32 s = (pos + ibal) & 3u;
+    const u32 c = __builtin_amdgcn_alignbyte(pd[1], pd[0], s) & 0xffu;
+    const u32 e = tagtab[c];
+    // bytes pos+1 .. pos+16 (a short literal's bytes; a copy's offset bytes)
+    const bool q = s == 3;
+    const u32 w0 = q ? pd[1] : pd[0], w1 = q ? pd[2] : pd[1], w2 = q ? pd[3] : pd[2];
+    const u32 w3 = q ? pd4 : pd[3];
+    const u32 b = (s + 1) & 3u;
+    const u32x4 xr = u32x4{__builtin_amdgcn_alignbyte(w1, w0, b), __builtin_amdgcn_alignbyte(w2, w1, b),
+                           __builtin_amdgcn_alignbyte(w3, w2, b), __builtin_amdgcn_alignbyte(pd4, w3, b)};
+    const u32 val = xr[0] & (0xffffffffu >> (e & 31u));
+    const bool is_lit = e & 64u;
+    const u32 len = (e & 32u) ? val + 1u : (e >> 8) & 0x7fu;
+    const u32 off = val + (e >> 20);
+    const u32 nb = (e >> 16) & 7u;
+    const u32 lsrc = pos + 1 + nb;
+
+    const u64 bigm = __ballot(valid && is_lit && len > 64);
+    if (bigm & 1ull) {
+      // ---------- long literal: written straight to the slot by the whole
+      // wave; the window restarts behind it (as v4)
+      const u32 L = readlane(len, 0), S = readlane(lsrc, 0);
+      if ((u64)op + L > op1) {
+        if (lane == 0) status[m] = kCorrupt;
+        return;
+      }
+      flush_to(op);
+      for (u32 k0 = 0; k0 < L; k0 += 4096) {
+        Raw16 x[4];
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) x[r] = raw_load16(irsrc, S + k0 + 1024 * r + lane * 16 + ibal);
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) {
+          const u32 k = k0 + 1024 * r + lane * 16;
+          if (k < L) store_exact(ob + op + k, shifted16(x[r]), L - k < 16 ? L - k : 16u);
+        }
+      }
+      op += L;
+      flushed = op;
+      sbase = (int)((op + obal) & ~15u) - (int)obal - 16;
+      zero_from(0);
+      zero_end = 1024;
+      wave_lds_fence();
+      if (lane < 2) {
+        const u32 lo = (u32)sbase + 16 * lane;
+        if (lo < op) {
+          const u32 cnt = op - lo < 16 ? op - lo : 16u;
+          store_exact(sb + 16 * lane, rsrc_load16(irsrc, S + L - (op - lo) + ibal), cnt);
+        }
+      }
+      wave_lds_fence();
+      head += 1;
+      pf_head = 0xffffffffu;
+      if (head == tail) {
+        const u32 nw = (S + L) >> 5;
+        if (nw > scan) {
+          scan = nw;
+          bmw = fill_word(scan);
+        }
+      }
+      continue;
+    }
+    const u32 take = bigm ? (u32)__builtin_ctzll(bigm) : take0;
+    const bool v = lane < take;
+
+    // ---------- output positions: <= kGroupBytes per group
+    const u32 lv = v ? len : 0u;
+    const u32 incl = dpp_incl_scan(lv);
+    const u32 t_op = op + incl - lv;
+    const bool fits = v && incl <= kGroupBytes && t_op < op1;
+    const u32 k_tags = (u32)__builtin_popcountll(__ballot(fits));
+    const u32 tot_len = readlane(incl, k_tags - 1);
+    // the writer's checks (snappy.cc:1166, :1200, :1400, :1410, :1466)
+    if (__any(fits && ((u64)t_op + len > op1 || (!is_lit && (off == 0 || off > t_op - op0))))) {
+      if (lane == 0) status[m] = kCorrupt;
+      return;
+    }
+
+    // ---------- slide the window if this group would overrun it (as v4)
+    if (op + tot_len - sbase > kWindow) {
+      const int nsb = (int)(((op - keep_hist + obal) & ~15u)) - (int)obal;
+      if ((int)flushed < nsb + 16) flush_to((u32)((int)((op + obal) & ~15u) - (int)obal));
+      wait_all_memory();
+      const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
+      for (u32 k = 0; k < keep; k += 1024) {
+        const u32 i = k + 16 * lane;
+        u32x4 x = u32x4{0, 0, 0, 0};
+        if (i < keep) x = *reinterpret_cast<const u32x4*>(sb + shift + i);
+        wave_lds_fence();
+        if (i < keep) *reinterpret_cast<u32x4*>(sb + i) = x;
+        wave_lds_fence();
+      }
+      sbase = nsb;
+      zero_end = (keep + 15) & ~15u;
+    }
+    // ---------- prefetch the next group's tag bytes
+    {
+      const u32 nh = head + k_tags;
+      const u32 na = tail - nh;
+      const u32 ncnt = na < 64 ? na : 64u;
+      if (lane < ncnt) prefetch(ring[(nh + lane) & (kTagRing - 1)]);
+      pf_head = nh;
+      pf_cnt = ncnt;
+    }
+    while (op + tot_len + 20 - sbase > zero_end) {
+      zero_from(zero_end);
+      zero_end += 1024;
+    }
+    wave_lds_fence();
+
+    // ---------- chunks: a literal's all come in round A (registers for
+    // chunk 0 of a short literal, else the input); a copy's leading chunks
+    // whose 16-byte source starts below the window base come from the slot
+    // (far: stored at least one group ago); the rest run in rounds B
+    const u32 src = is_lit ? lsrc : t_op - off;
+    const u32 nch = (len + 15) >> 4;
+    const bool pat = !is_lit && off < 16 && off < len;
+    u32 kf = 0;
+    if (fits) {
+      if (is_lit) {
+        kf = nch;
+      } else if (!pat && (int)src < sbase) {
+        const u32 kfar = (((u32)(sbase - (int)src) - 1) >> 4) + 1;
+        kf = kfar < nch ? kfar : nch;
+      }
+    }
+    const bool reg0 = is_lit && nb == 0;
+    // Loads only here: the data is first used after the flush below, so all
+    // of a lane's chunk loads are in flight together.  A literal chunk is a
+    // 16- and a 4-byte load at the dword below it, shifted later by sh; a far
+    // chunk one unaligned 16-byte load (shift 0).
+    const u32 sh = is_lit ? (src + ibal) & 3u : 0u;
+    auto gload = [&](u32 k, u32x4& d, u32& d4) {
+      if (is_lit) {
+        const u32 a = (src + 16 * k + ibal) & ~3u;
+        d = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
+        d4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
+      } else {
+        d = far_load(orsrc, src + 16 * k + obal);
+      }
+    };
+    auto shf = [&](const u32x4& d, u32 d4, u32 t) {
+      return u32x4{__builtin_amdgcn_alignbyte(d[1], d[0], t), __builtin_amdgcn_alignbyte(d[2], d[1], t),
+                   __builtin_amdgcn_alignbyte(d[3], d[2], t), __builtin_amdgcn_alignbyte(d4, d[3], t)};
+    };
+    u32x4 a0 = xr, a1 = u32x4{0, 0, 0, 0};
+    u32 a0e = 0, a1e = 0;
+    if (kf > 0 && !reg0) gload(0, a0, a0e);
+    const u64 m1 = __ballot(kf > 1);
+    if (m1 && kf > 1) gload(1, a1, a1e);
+    if (prio) __builtin_amdgcn_s_setprio(0);
+    {  // the previous groups' completed blocks, while the loads are in flight
+      const int fe = (int)((op + obal) & ~15u) - (int)obal;
+      if (fe >= (int)flushed + 1024) flush_to((u32)fe);
+    }
+    const u32 wa = (u32)((int)t_op - sbase);
+    if (kf > 0) or_store(sb, wa, shf(a0, a0e, reg0 ? 0u : sh), len < 16 ? len : 16u, mtab);
+    if (m1) {
+      if (kf > 1) or_store(sb, wa + 16, shf(a1, a1e, sh), len - 16 < 16 ? len - 16 : 16u, mtab);
+      // chunks 2-3 (literals and far copies of 33..64 bytes: rare) reuse the
+      // registers, one more round trip
+      if (__ballot(kf > 2)) {
+        if (kf > 2) gload(2, a0, a0e);
+        if (kf > 3) gload(3, a1, a1e);
+        if (kf > 2) or_store(sb, wa + 32, shf(a0, a0e, sh), len - 32 < 16 ? len - 32 : 16u, mtab);
+        if (kf > 3) or_store(sb, wa + 48, shf(a1, a1e, sh), len - 48, mtab);
+      }
+    }
+    wave_lds_fence();
+
+    // ---------- rounds B: near chunks, in LDS, in dependency order
+    u32 rem = (fits && kf < nch) ? len - 16 * kf : 0u;
+    u32 cd = t_op + 16 * kf, cs = src + 16 * kf;
+    const u32 stp = pat ? pat_step(off) : 16u;
+    bool pf = pat;
+    u64 pend = __ballot(rem > 0);
+    while (pend) {
+      const u32 W = readlane(cd, (u32)__builtin_ctzll(pend));
+      const u32 n = rem < stp ? rem : stp;
+      const u32 ne = pf ? cd : cs + n;
+      if (rem > 0 && ne <= W) {
+        u32x4 x = lds_read16(sb + ((int)cs - sbase));
+        if (pf) x = expand_pattern(x, off, sel_tab);
+        or_store(sb, (u32)((int)cd - sbase), x, n, mtab);
+        rem -= n;
+        cd += n;
+        cs = pat ? cd - stp : cs + n;
+        pf = false;
+      }
+      wave_lds_fence();
+      pend = __ballot(rem > 0);
+    }
+    op += tot_len;
+    head += k_tags;
+  }
+  if (op != op1) {  // the stream ended early (snappy.cc:858-868)
+    if (lane == 0) status[m] = kCorrupt;
+    return;
+  }
+  flush_to(op1);
+}
+
 // 6 waves per SIMD (62 VGPRs, LDS 25 KB per block); 7 waves (smaller tag ring
 // or window) and larger windows at 3-4 waves were slower.
 // The first kBigBlocks blocks take the large messages listed by pass 1 from a
 // device counter (blocks dispatch in order, so the longest messages start
 // first); every other block runs the wave-per-message mapping and skips them.
 // (A fully persistent grid was measured slower on uniform batches.)
+template <int V>
 __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_per_eu(6, 6))) void exec_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, u8* out,
@@ -1144,12 +1577,26 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
   // per wave: the tag ring, then the output window; a large message's index
   // walk stages its input over both (kBigStageBytes + 16 <= their size)
   __shared__ __attribute__((aligned(16))) u8 wl_s[kWavesPerBlock][4 * kTagRing + kWindow + 32];
-  __shared__ __attribute__((aligned(16))) u8 pmap_s[kWavesPerBlock][kMaxPieces];
+  __shared__ __attribute__((aligned(16))) u8 pmap_s[kWavesPerBlock][V == 5 ? 1 : kMaxPieces];
   __shared__ u32x4 sel_tab[16];
+  __shared__ u32 tagtab[V == 5 ? 256 : 1];
+  __shared__ u32x4 mask_tab[17];
   static_assert(kBigStageBytes + 16 <= 4 * kTagRing + kWindow + 32, "stage fits the wave's LDS");
+  static_assert(kWavesPerBlock * 64 == 256, "one tag table entry per thread");
 
   if (threadIdx.x < 64) init_pattern_table(sel_tab, threadIdx.x);
+  if constexpr (V == 5) tagtab[threadIdx.x] = exec_tag_entry(threadIdx.x);
+  init_mask_table(mask_tab, threadIdx.x);
   __syncthreads();
+  // one message (or segment) with the pass-2 variant V
+  auto run = [&](u32 m, u32* ring, u8* pmap, u8* sb, u32 lane, i32 st, u32 ip0, u32 op0, u32 op1) {
+    if constexpr (V == 5)
+      exec5_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, tagtab,
+                    sb, sel_tab, mask_tab, lane, st, ip0, op0, op1, prio != 0, keep_hist);
+    else
+      exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, pmap,
+                   sb, sel_tab, mask_tab, lane, st, ip0, op0, op1, prio != 0, keep_hist);
+  };
 
   // wave index made visibly uniform: the message's sizes, pointers and the
   // walk state (head, tail, op, window base) then live in SGPRs and branches
@@ -1162,9 +1609,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
 
   if (blockIdx.x >= big_blocks) {
     const u32 m = (blockIdx.x - big_blocks) * kWavesPerBlock + wv;
-    if (m < n_msgs && in_len[m] <= big_threshold)
-      exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring,
-                   pmap, sb, sel_tab, lane, status[m], 0u, 0u, out_len[m], prio != 0, keep_hist);
+    if (m < n_msgs && in_len[m] <= big_threshold) run(m, ring, pmap, sb, lane, status[m], 0u, 0u, out_len[m]);
     return;
   }
   // large messages, listed by pass 1b: whole ones first (the longest start
@@ -1181,8 +1626,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     if (idx >= total) break;
     if (idx < n_whole) {
       const u32 m = whole_list[idx];
-      exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring,
-                   pmap, sb, sel_tab, lane, status[m], 0u, 0u, out_len[m], prio != 0, keep_hist);
+      run(m, ring, pmap, sb, lane, status[m], 0u, 0u, out_len[m]);
       continue;
     }
     const u64 e = segs[idx - n_whole];
@@ -1194,8 +1638,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     const u32 op1 = (e >> 63) ? expected : op0 + 65536u;
     u32 ip0 = 0;  // segment k > 0 starts at the input offset pass 1b left in its slot
     if (k) __builtin_memcpy(&ip0, out + out_off[m] + op0, 4);
-    exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, pmap,
-                 sb, sel_tab, lane, status[m], ip0, op0, op1, prio != 0, keep_hist);
+    run(m, ring, pmap, sb, lane, status[m], ip0, op0, op1);
   }
 }
 
@@ -1247,6 +1690,7 @@ size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
 struct SideStream {
   hipStream_t stream = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t pass1 = nullptr;  // two-stream calls: pass 1 done (fsg_decompress_batch_2s)
   std::mutex mu;
 };
 static SideStream* side_stream() {
@@ -1259,7 +1703,8 @@ static SideStream* side_stream() {
   std::call_once(g_once[dev], [s] {
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&s->fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&s->join, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&s->join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->pass1, hipEventDisableTiming) != hipSuccess)
       s->stream = nullptr;
   });
   return s->stream ? s : nullptr;
@@ -1268,8 +1713,21 @@ static SideStream* side_stream() {
 hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u8* out, const u64* out_off,
                             const u32* out_cap, u32* out_len, i32* status,
-                            u32 flags, void* ws, size_t ws_bytes, hipStream_t stream) {
+                            u32 flags, void* ws, size_t ws_bytes, hipStream_t stream,
+                            int exec_variant, hipStream_t pass1_stream) {
   if (n_msgs == 0) return hipSuccess;
+  // Two-stream form: pass 1 (fill, lane walk, pass 1b) on pass1_stream, pass 2
+  // (exec, fallback) on `stream` behind an event, so a caller's next batch
+  // (its own workspace and outputs) can walk while this one executes.
+  SideStream* two = nullptr;
+  if (pass1_stream && pass1_stream != stream) {
+    two = side_stream();
+    if (!two) return hipErrorNotReady;
+  }
+  hipStream_t const caller_stream = stream;
+  if (two) stream = pass1_stream;  // every pass-1 launch below goes there
+  // pass 2: one tag per lane (5) or <= 16-byte pieces per lane (4)
+  auto* const ek = exec_variant == 4 ? &exec_kernel<4> : &exec_kernel<5>;
   u8* w = static_cast<u8*>(ws);
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
   if (ws_bytes < 256 + kListBases * base_bytes + 4 * 64) return hipErrorInvalidValue;
@@ -1330,15 +1788,15 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     return e && e[0] == '0' ? 0u : 1u;
   }();
   // history kept when an exec window slides (FSG_EXEC_KEEP, read per call:
-  // the tests shrink it to exercise the slide's flush rule; 512..3072 bytes,
-  // a multiple of 16)
+  // the tests shrink it to exercise the slide's flush rule; 512..kMaxKeep
+  // bytes, a multiple of 16)
   u32 keep_hist = kKeep;
   if (const char* ke = getenv("FSG_EXEC_KEEP")) {
     const int v = atoi(ke);
-    if (v >= 512 && v <= 3072 && v % 16 == 0) keep_hist = (u32)v;
+    if (v >= 512 && v <= (int)kMaxKeep && v % 16 == 0) keep_hist = (u32)v;
   }
   const char* fork_env = getenv("FSG_DECODE_FORK");  // read per call: tests set it
-  const bool fork = fork_env ? atoi(fork_env) != 0 : n_msgs > 131072u;
+  const bool fork = !two && (fork_env ? atoi(fork_env) != 0 : n_msgs > 131072u);
   const u32 big_blocks = small_blocks < kBigBlocks ? small_blocks : kBigBlocks;
   auto launch_index_big = [&](hipStream_t st) -> hipError_t {
     // pass 1b: large messages, one wave each (an empty list costs one short
@@ -1356,7 +1814,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     if (e2 != hipSuccess) return e2;
     // the large-message blocks only (exit after one atomic when the lists
     // are empty)
-    exec_kernel<<<big_blocks, kWavesPerBlock * 64, 0, st>>>(
+    ek<<<big_blocks, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
         reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), big_blocks, big_threshold, 0u,
@@ -1366,7 +1824,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   auto launch_small = [&](hipStream_t st) -> hipError_t {
     // one wave per message; large ones are skipped (big_blocks = 0: no block
     // takes the large-message role)
-    exec_kernel<<<small_blocks, kWavesPerBlock * 64, 0, st>>>(
+    ek<<<small_blocks, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
         reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), 0u, big_threshold, 0u,
@@ -1395,7 +1853,13 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     // per wave
     if ((e = launch_index(false)) != hipSuccess) return e;
     if ((e = launch_index_big(stream)) != hipSuccess) return e;
-    exec_kernel<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(
+    if (two) {
+      std::lock_guard<std::mutex> lk(two->mu);
+      if ((e = hipEventRecord(two->pass1, stream)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(caller_stream, two->pass1, 0)) != hipSuccess) return e;
+      stream = caller_stream;
+    }
+    ek<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
         reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), big_blocks,

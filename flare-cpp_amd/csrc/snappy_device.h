@@ -70,6 +70,7 @@ __device__ __forceinline__ void stu64(u8* p, u64 v) { __builtin_memcpy(p, &v, 8)
 __device__ __forceinline__ void stu32(u8* p, u32 v) { __builtin_memcpy(p, &v, 4); }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void copy16(u8* d, const u8* s) {
   u32x4 v;
   __builtin_memcpy(&v, s, 16);

@@ -93,6 +93,7 @@ int fsh_cpu_lz4_uncompress(const uint8_t* in, size_t n, uint8_t* out, size_t cap
   const size_t h = flare::lz4::cpu::ReadHeader(in, n, ulen);
   if (h == 0) return -1;
   if (*ulen > cap) return -2;
+  if (!flare::lz4::cpu::PlausibleLength(*ulen, n - h)) return 0;
   return flare::lz4::cpu::DecompressBlock(in + h, n - h, out, *ulen) ? 1 : 0;
 }
 

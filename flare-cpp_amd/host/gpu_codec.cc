@@ -503,7 +503,9 @@ struct SnappyGpuCodec::Impl {
   std::deque<Request*> queue;
   std::vector<std::unique_ptr<Device>> devs;
   std::vector<char> busy;
-  bool started = false;
+  // double-checked start: read without the lock on every handler call,
+  // published with release once start_locked has set the devices up
+  std::atomic<bool> started{false};
   std::string err;
   std::atomic<int> n_devs{0};
   std::atomic<size_t> min_bytes{env_min_bytes()};
@@ -511,13 +513,18 @@ struct SnappyGpuCodec::Impl {
   Counters ctr;
 
   void ensure_started() {
-    if (started) return;  // racy read is fine: start() re-checks under the lock
+    if (started.load(std::memory_order_acquire)) return;
     std::unique_lock<std::mutex> lk(mu);
-    if (!started) start_locked(env_device_mask());
+    if (!started.load(std::memory_order_relaxed)) start_locked(env_device_mask());
   }
 
   int start_locked(uint64_t mask) {
-    started = true;
+    const int n = start_devices_locked(mask);
+    started.store(true, std::memory_order_release);
+    return n;
+  }
+
+  int start_devices_locked(uint64_t mask) {
     err.clear();
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
@@ -726,7 +733,7 @@ void SnappyGpuCodec::Shutdown() {
   std::unique_lock<std::mutex> lk(impl_->mu);
   impl_->quiesce(lk);
   impl_->stop_locked();
-  impl_->started = true;  // stay on the host codec until InitDevices
+  impl_->started.store(true, std::memory_order_release);  // stay on the host codec until InitDevices
   impl_->err = "shut down";
 }
 

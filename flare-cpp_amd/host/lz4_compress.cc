@@ -25,7 +25,9 @@ bool Lz4Decompress(const cord_buf& in, cord_buf* out) {
   in.copy_to(body.data(), n);
   uint32_t ulen = 0;
   const size_t h = lz4::cpu::ReadHeader(body.data(), n, &ulen);
-  if (h == 0) return false;
+  // the header comes from the peer: bound it by what the block can hold
+  // before allocating (a 5-byte body may claim 4 GiB)
+  if (h == 0 || !lz4::cpu::PlausibleLength(ulen, n - h)) return false;
   std::vector<uint8_t> raw(ulen);
   if (!lz4::cpu::DecompressBlock(body.data() + h, n - h, raw.data(), ulen)) return false;
   return out->append(raw.data(), ulen) == 0;

@@ -19,6 +19,14 @@ constexpr size_t kMaxInput = 0x7E000000;  // LZ4_MAX_INPUT_SIZE
 inline size_t BlockBound(size_t n) { return n + n / 255 + 16; }
 inline size_t MaxCompressedLength(size_t n) { return 5 + BlockBound(n); }
 
+// The most a valid block of n bytes can decode to: every byte of a length
+// extension adds at most 255 output bytes, a token with its 2-byte offset at
+// most 34.  A body whose header claims more is rejected before anything is
+// allocated for it.
+inline bool PlausibleLength(uint64_t ulen, size_t block_bytes) {
+  return ulen <= 255ull * block_bytes + 64;
+}
+
 // One block of n <= kMaxInput bytes into out (BlockBound(n) bytes); returns
 // its length.
 size_t CompressBlock(const uint8_t* in, size_t n, uint8_t* out);

@@ -38,6 +38,8 @@ _SIGS = {
     "fsg_decompress_workspace_bytes": (_sz, [_u32, _u64]),
     "fsg_compress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "fsg_decompress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
+    "fsg_decompress_batch_2s": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp,
+                                           _vp]),
     "fsg_lz4_max_compressed_length": (_sz, [_sz]),
     "fsg_lz4_compress_workspace_bytes": (_sz, [_u32]),
     "fsg_lz4_compress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
@@ -53,12 +55,18 @@ def header_symbols(header: Path | None = None) -> list[str]:
     return sorted(set(re.findall(r"\b(fsg_[a-z0-9_]+)\s*\(", text)))
 
 
+# entry points an older library under A/B may lack
+_OPTIONAL = {"fsg_decompress_batch_2s"}
+
+
 def load_gpu_lib(path: Path | None = None) -> ctypes.CDLL:
     path = Path(path or os.environ.get("FSG_LIB", LIB_DIR / "libflare_snappy_gpu.so"))
     if not path.exists():
         raise RuntimeError(f"HIP codec library missing: {path} (run __graft_entry__.build())")
     lib = ctypes.CDLL(str(path))
     for name, (res, args) in _SIGS.items():
+        if name in _OPTIONAL and not hasattr(lib, name):
+            continue  # an older build under A/B (FSG_LIB)
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
     return lib
@@ -117,12 +125,18 @@ class SnappyGPU:
             self._stream(stream)), "fsg_compress_batch")
 
     def decompress(self, d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len,
-                   d_status, flags=0, stream=None, workspace=None):
+                   d_status, flags=0, stream=None, workspace=None, pass1_stream=None):
+        """fsg_decompress_batch; with `pass1_stream`, fsg_decompress_batch_2s
+        (the tag walk on pass1_stream, the execution on `stream`)."""
         ws = 0 if workspace is None else workspace.numel() * workspace.element_size()
-        self._check(self.lib.fsg_decompress_batch(
-            _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off),
-            _ptr(d_out_cap), _ptr(d_out_len), _ptr(d_status), flags, _ptr(workspace), ws,
-            self._stream(stream)), "fsg_decompress_batch")
+        args = (_ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off),
+                _ptr(d_out_cap), _ptr(d_out_len), _ptr(d_status), flags, _ptr(workspace), ws,
+                self._stream(stream))
+        if pass1_stream is None:
+            self._check(self.lib.fsg_decompress_batch(*args), "fsg_decompress_batch")
+        else:
+            self._check(self.lib.fsg_decompress_batch_2s(*args, self._stream(pass1_stream)),
+                        "fsg_decompress_batch_2s")
 
     # ---- LZ4 (include/flare_lz4_gpu.h)
     def lz4_compress_workspace(self, n, device=None):

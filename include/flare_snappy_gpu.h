@@ -88,7 +88,10 @@ const char *fsg_last_error(void);
  * two-pass decoder (lane-per-message index pass writing a tag-start bitmap,
  * then one wave per message executing <= 16-byte pieces in dependency rounds
  * through an LDS output window), the default decoder whenever the workspace
- * holds its bitmap.  (Generation 2 was retired; 2 is rejected.)  Every
+ * holds its bitmap, 5 = decode only: the same two passes with one TAG per
+ * lane in the execution pass (registers hold a short literal's bytes from the
+ * tag prefetch; no piece map), the default since round 3.  (Generation 2 was
+ * retired; 2 is rejected.)  Every
  * variant produces identical bytes and statuses.  Process-wide; not for use
  * while other threads launch batches. */
 int fsg_select_kernels(int decode_variant, int encode_variant);
@@ -167,6 +170,23 @@ int fsg_decompress_batch(const uint8_t *d_in, const uint64_t *d_in_off,
                          const uint32_t *d_out_cap, uint32_t *d_out_len,
                          int32_t *d_status, uint32_t flags, void *d_workspace,
                          size_t workspace_bytes, void *stream);
+
+/* fsg_decompress_batch with its two passes on two streams: pass 1 (header
+ * checks, the tag walk, the tag-start bitmap) runs on `pass1_stream`, pass 2
+ * (execution) on `stream` after pass 1 (an event).  Same bytes and statuses.
+ * A caller decoding a stream of batches alternates two sets of
+ * workspace / output / d_out_len / d_status buffers, so batch k+1's pass 1
+ * runs beside batch k's pass 2 (the tag walk is latency-bound, the execution
+ * issue-bound).  The inputs must be ready on `pass1_stream`; calls that share
+ * any of those buffers must be ordered by the caller (pass 1 writes the
+ * workspace, d_out_len, d_status and, for messages cut into 64 KiB segments,
+ * 4 bytes of d_out).  Results are valid once `stream` is synchronised. */
+int fsg_decompress_batch_2s(const uint8_t *d_in, const uint64_t *d_in_off,
+                            const uint32_t *d_in_len, uint32_t n_msgs,
+                            uint8_t *d_out, const uint64_t *d_out_off,
+                            const uint32_t *d_out_cap, uint32_t *d_out_len,
+                            int32_t *d_status, uint32_t flags, void *d_workspace,
+                            size_t workspace_bytes, void *stream, void *pass1_stream);
 
 #ifdef __cplusplus
 }

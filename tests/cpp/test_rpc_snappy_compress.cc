@@ -129,6 +129,11 @@ TEST_CPU(lz4_handler) {
   cord_buf bad;
   bad.append(std::string("\x05\x50hel", 5));  // literals cut short
   ASSERT_FALSE(policy::Lz4Decompress(bad, &back));
+  // a tiny body whose header claims 0xFFFFFFFF bytes: rejected by the length
+  // bound before anything is allocated for it (no bad_alloc out of the handler)
+  cord_buf huge;
+  huge.append(std::string("\xff\xff\xff\xff\x0f\x10\x61", 7));
+  ASSERT_FALSE(policy::Lz4Decompress(huge, &back));
 }
 
 TEST_CPU(cord_buf_blocks) {

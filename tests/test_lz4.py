@@ -124,6 +124,16 @@ def test_host_codec_blocks_equal_fixtures_and_oracle(host, o):
         assert r == 1 and y == x, v["name"]
 
 
+def test_host_codec_rejects_implausible_header(host):
+    # a 2-byte block cannot decode to 4 GiB: the header is refused before
+    # any output is sized from it (the drop-in's Lz4Decompress does the same)
+    body = bytes([0xFF, 0xFF, 0xFF, 0xFF, 0x0F, 0x10, 0x61])
+    r, _, _ = _host_uncompress(host, body, 1 << 20)
+    assert r != 1
+    r, ulen, _ = _host_uncompress(host, bytes([0xFF, 0xFF, 0x03, 0x10, 0x61]), 1 << 20)
+    assert r == 0 and ulen == 0xFFFF  # fits the cap, exceeds 255 x 2 + 64: invalid
+
+
 def test_host_codec_verdicts_equal_oracle(host, o):
     rng = np.random.default_rng(23)
     src = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (30, 700, 9000)]

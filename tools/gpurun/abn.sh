@@ -3,7 +3,7 @@
 # twice over, on the workloads in $WLS (default C3 decode).  An entry
 # name@VAR=value runs lib_<name>.so with that environment variable set.
 mkdir -p gpurun_out/abn
-B="python bench.py --no-cpu-baseline --no-e2e --no-encode --steps 10 --warmup 2 --verify-sample 16"
+B="python bench.py --no-cpu-baseline --no-e2e --no-encode --pipeline 0 --steps 10 --warmup 2 --verify-sample 16"
 for w in ${WLS:-c3-decompress}; do
   for pass in 1 2; do
     for e in $LIBS; do
