@@ -91,7 +91,7 @@ def parse(argv=None):
     ap.add_argument("--scaling", choices=["weak", "strong"], default=None,
                     help="weak: every GPU owns a full batch; strong: one batch split by bytes "
                          "(default: per workload, strong for cm/c5)")
-    ap.add_argument("--pipeline", type=int, default=1,
+    ap.add_argument("--pipeline", type=int, default=0,
                     help="decompress on a GPU: time a stream of two alternating batches, batch k+1's "
                          "tag walk (pass 1, its own stream) beside batch k's execution "
                          "(fsg_decompress_batch_2s); 0 = one batch, both passes on one stream")

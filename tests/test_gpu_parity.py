@@ -193,7 +193,7 @@ def test_large_message_index_fuzz(gpu, oracle, fork, monkeypatch):
             assert s == fsg.FSG_OK and o[:ulen] == ref, i
 
 
-@pytest.mark.parametrize("variant", [1, 3, 4])
+@pytest.mark.parametrize("variant", [1, 3, 4, 5])
 def test_kernel_variants_agree(gpu, oracle, variant):
     """Every generation of kernels gives the oracle's bytes and statuses."""
     gpu.codec.select_kernels(variant, min(variant, 3))
@@ -433,21 +433,27 @@ def test_large_message_segments(gpu, oracle, fork, monkeypatch):
         assert s == fsg.FSG_OK and o[:ulen] == ref, (i, s)
 
 
-def test_far_copies_at_window_edge(gpu, oracle):
+@pytest.mark.parametrize("variant,rule", [(5, "tags"), (4, "pieces")])
+def test_far_copies_at_window_edge(gpu, oracle, variant, rule):
     """Copies whose sources lie a few bytes either side of pass 2's window base
     (tests/window_edge.py replays the kernel's group/window rules to place
-    them): far copies read back output stored to global memory in earlier
-    groups, including 16-byte loads straddling the base, right after window
-    slides and long-literal restarts.  Decoded bytes equal the construction's
-    and the oracle's, messages side by side in 16-byte-aligned slots."""
+    them, per execution pass: one tag per lane, or <= 16-byte pieces): far
+    copies read back output stored to global memory in earlier groups,
+    including 16-byte loads straddling the base, right after window slides
+    and long-literal restarts.  Decoded bytes equal the construction's and
+    the oracle's, messages side by side in 16-byte-aligned slots."""
     from window_edge import edge_stream
     rng = np.random.default_rng(31)
     comps, raws, n_edge = [], [], 0
     for i in range(800):
-        c, raw, e = edge_stream(rng, int(rng.integers(2000, 40000)))
+        c, raw, e = edge_stream(rng, int(rng.integers(2000, 40000)), rule=rule)
         comps.append(c); raws.append(raw); n_edge += e
     assert n_edge > 5000
-    outs, ol, st = gpu.decompress(comps, [len(r) for r in raws])
+    gpu.codec.select_kernels(variant, 0)
+    try:
+        outs, ol, st = gpu.decompress(comps, [len(r) for r in raws])
+    finally:
+        gpu.codec.select_kernels(0, 0)
     for i, (c, raw, o, s) in enumerate(zip(comps, raws, outs, st)):
         assert s == fsg.FSG_OK and o == raw, i
     for i in range(0, 800, 97):
@@ -524,3 +530,76 @@ def test_window_slide_flush_rule(gpu, oracle, keep, monkeypatch):
     outs, ol, st = gpu.decompress(comps, [len(d) for d in datas])
     for i, (d, o, s) in enumerate(zip(datas, outs, st)):
         assert s == fsg.FSG_OK and o == d, i
+
+
+def test_two_stream_decode_stream_of_batches(gpu, oracle):
+    """fsg_decompress_batch_2s: pass 1 on a second stream, pass 2 on the
+    caller's, over a stream of distinct batches alternating two buffer sets
+    (batch k+1's tag walk beside batch k's execution; a set is reused only
+    after its previous execution, by an event).  Every batch's bytes and
+    statuses equal the oracle's: small and large bodies (the segment path),
+    random bodies and corrupt ones."""
+    import torch
+    from gpu_harness import dev
+    rng = np.random.default_rng(77)
+    batches = []
+    for k in range(6):
+        srcs = [fsg.make_batch(fsg.KIND_TEXT, [int(s)], first_index=1000 * k + j).item(0)
+                for j, s in enumerate(rng.integers(1, 70000, 40))]
+        srcs.append(fsg.make_batch(fsg.KIND_TEXT, [200000 + k], first_index=k).item(0))
+        srcs.append(fsg.make_batch(fsg.KIND_RANDOM, [5000], first_index=k).item(0))
+        comps = [oracle.compress(s) for s in srcs]
+        bad = bytearray(comps[3])
+        bad[len(bad) // 2] ^= 0x77
+        comps.append(bytes(bad))
+        batches.append(comps)
+    codec = gpu.codec
+    s_main = torch.cuda.current_stream()
+    s1 = torch.cuda.Stream()
+    sets = []
+    for k, comps in enumerate(batches):
+        b = fsg.Batch.from_list(comps)
+        caps = np.full(len(b), 1 << 18, dtype=np.uint32)
+        oo, tot = fsg.slot_offsets(caps.astype(np.uint64))
+        sets.append(dict(n=len(b), d_in=dev(b.data), d_io=dev(b.offsets), d_il=dev(b.lens), oo=oo, d_oo=dev(oo),
+                         d_cap=dev(caps), caps=caps))
+    slot_bufs = []
+    for _ in range(2):
+        n = max(s["n"] for s in sets)
+        slot_bufs.append(dict(out=torch.zeros(n << 18, dtype=torch.uint8, device="cuda"),
+                              ol=torch.zeros(n, dtype=torch.int32, device="cuda"),
+                              st=torch.full((n,), -7, dtype=torch.int32, device="cuda"),
+                              ws=codec.decompress_workspace(n, max(int(s["d_in"].numel()) for s in sets)),
+                              done=None))
+    torch.cuda.synchronize()
+    results = []
+
+    def collect(k):
+        sl = slot_bufs[k % 2]
+        s = sets[k]
+        torch.cuda.synchronize()
+        out = sl["out"].cpu().numpy()
+        ol = sl["ol"].cpu().numpy()[:s["n"]].view(np.uint32)
+        st = sl["st"].cpu().numpy()[:s["n"]]
+        results.append((k, [out[int(s["oo"][i]):int(s["oo"][i]) + int(min(ol[i], s["caps"][i]))].tobytes()
+                            for i in range(s["n"])], st.copy()))
+
+    for k, s in enumerate(sets):
+        sl = slot_bufs[k % 2]
+        if sl["done"] is not None:
+            collect(k - 2)  # (also orders: the set is free again)
+            s1.wait_event(sl["done"])
+        codec.decompress(s["d_in"], s["d_io"], s["d_il"], s["n"], sl["out"], s["d_oo"], s["d_cap"], sl["ol"],
+                         sl["st"], stream=s_main, workspace=sl["ws"], pass1_stream=s1)
+        ev = torch.cuda.Event()
+        ev.record(s_main)
+        sl["done"] = ev
+    collect(len(sets) - 2)
+    collect(len(sets) - 1)
+    assert sorted(r[0] for r in results) == list(range(len(sets)))
+    for k, outs, st in results:
+        for i, c in enumerate(batches[k]):
+            ok, ulen, ref = oracle.uncompress(c, cap=1 << 18)
+            assert (st[i] == fsg.FSG_OK) == bool(ok), (k, i, st[i])
+            if ok:
+                assert outs[i][:ulen] == ref, (k, i)

@@ -19,6 +19,15 @@ def test_window_model_rules():
     # a long literal runs alone and restarts the window below its end
     sb, pos = window_model([(True, 10, 0), (True, 100, 0), (False, 8, 20)])
     assert sb[2] == ((110 & ~15) - 16)
+    # the first slide comes before the group that would pass 4096: one tag per
+    # lane cuts groups at 1,024 output bytes (51 x 20-byte literals), pieces
+    # at 64 pieces (32 x two-piece literals)
+    tags = [(True, 20, 0)] * 400
+    for rule, per_group in (("tags", 51), ("pieces", 32)):
+        sb, pos = window_model(tags, rule)
+        first_slide = next(i for i, s in enumerate(sb) if s)
+        assert first_slide % per_group == 0, rule
+        assert pos[first_slide] + 20 * per_group > 4096 >= pos[first_slide], rule
 
 
 def test_edge_streams_valid():
@@ -26,7 +35,7 @@ def test_edge_streams_valid():
     rng = np.random.default_rng(8)
     n_edge = 0
     for i in range(60):
-        c, raw, e = edge_stream(rng, int(rng.integers(3000, 30000)))
+        c, raw, e = edge_stream(rng, int(rng.integers(3000, 30000)), rule="tags" if i % 2 else "pieces")
         ok, ulen, ref = o.uncompress(c, cap=len(raw))
         assert ok and ref == raw, i
         n_edge += e

@@ -8,8 +8,11 @@ copy reads the window (rounds B).  `window_model` replays the kernel's group
 and window rules on a tag list:
 
   * a group is the next <= 64 tags, cut before a literal longer than 64 bytes
-    and where the group's pieces (ceil(len / 16), or the pattern piece count
-    for offsets < 16) would pass 64;
+    and, for the default execution pass (decode variant 5, one tag per lane,
+    rule "tags"), where the group's output would pass 1,024 bytes; for the
+    piece-per-lane pass (variant 4, rule "pieces") where the group's pieces
+    (ceil(len / 16), or the pattern piece count for offsets < 16) would pass
+    64;
   * a literal longer than 64 bytes runs alone, and the window restarts one
     block below the block holding the new write position:
     sbase = (op & ~15) - 16;
@@ -26,7 +29,7 @@ from __future__ import annotations
 
 import numpy as np
 
-WINDOW, KEEP, MAX_PIECES = 4096, 2048, 64
+WINDOW, KEEP, MAX_PIECES, GROUP_BYTES = 4096, 2048, 64, 1024
 
 
 def _pieces(ln: int, off: int) -> int:
@@ -36,9 +39,10 @@ def _pieces(ln: int, off: int) -> int:
     return -(-ln // 16)
 
 
-def window_model(tags):
+def window_model(tags, rule: str = "tags"):
     """tags: list of (is_literal, length, offset).  Returns, per tag, the
-    window base (sbase) in force when its group runs and its output position."""
+    window base (sbase) in force when its group runs and its output position.
+    rule: "tags" (decode variant 5) or "pieces" (variant 4)."""
     sb = [0] * len(tags)
     pos = [0] * len(tags)
     op, sbase, i = 0, 0, 0
@@ -55,8 +59,8 @@ def window_model(tags):
             l2, n2, o2 = tags[j]
             if l2 and n2 > 64:
                 break
-            p = _pieces(n2, 0 if l2 else o2)
-            if pc + p > MAX_PIECES:
+            p = _pieces(n2, 0 if l2 else o2) if rule == "pieces" else 0
+            if pc + p > MAX_PIECES or (rule == "tags" and tot + n2 > GROUP_BYTES):
                 break
             pc += p
             tot += n2
@@ -85,7 +89,7 @@ def _emit_copy(off: int, ln: int) -> bytes:
     return bytes([((ln - 1) << 2) | 2]) + off.to_bytes(2, "little")
 
 
-def edge_stream(rng, target: int, spread: int = 24):
+def edge_stream(rng, target: int, spread: int = 24, rule: str = "tags"):
     """(compressed, raw, n_edge): a valid stream of ~target output bytes whose
     copies read from sbase - spread .. sbase + spread of their group (when the
     output so far allows), plus the count of copies whose 16-byte source load
@@ -104,7 +108,7 @@ def edge_stream(rng, target: int, spread: int = 24):
             ln = int(rng.integers(4, 65))
             tags.append((False, ln, 16))          # offset fixed below (>= 16)
         n += ln
-    sb, pos = window_model(tags)
+    sb, pos = window_model(tags, rule)
     out = bytearray()
     body = []
     n_edge = 0
