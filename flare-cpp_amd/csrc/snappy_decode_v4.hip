@@ -1282,6 +1282,10 @@ __device__ __forceinline__ void exec5_message(
   }
   const u32* bm = bitmap + bmb;
   const u32 nwords = (n_in + 31) >> 5;
+#ifdef FSG_STAMPS
+  u64 st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 t_last_ = __builtin_amdgcn_s_memtime();
+#endif
 
   u32 head = 0, tail = 0, scan = ip0 >> 5, op = op0;
   int sbase = (int)((op0 + obal) & ~15u) - (int)obal;  // output position of sb[0]
@@ -1343,6 +1347,7 @@ __device__ __forceinline__ void exec5_message(
       scan += kFillWords;
       bmw = fill_word(scan);
       wave_lds_fence();
+      STAMP(0);
       continue;
     }
     const u32 avail = tail - head;
@@ -1374,6 +1379,7 @@ __device__ __forceinline__ void exec5_message(
     const u32 lsrc = pos + 1 + nb;
 
     const u64 bigm = __ballot(valid && is_lit && len > 64);
+    STAMP(1);
     if (bigm & 1ull) {
       // ---------- long literal: written straight to the slot by the whole
       // wave; the window restarts behind it (as v4)
@@ -1416,6 +1422,7 @@ __device__ __forceinline__ void exec5_message(
           bmw = fill_word(scan);
         }
       }
+      STAMP(7);
       continue;
     }
     const u32 take = bigm ? (u32)__builtin_ctzll(bigm) : take0;
@@ -1466,6 +1473,7 @@ __device__ __forceinline__ void exec5_message(
     }
     wave_lds_fence();
 
+    STAMP(2);
     // ---------- chunks: a literal's all come in round A (registers for
     // chunk 0 of a short literal, else the input); a copy's leading chunks
     // whose 16-byte source starts below the window base come from the slot
@@ -1507,11 +1515,16 @@ __device__ __forceinline__ void exec5_message(
     const u64 m1 = __ballot(kf > 1);
     if (m1 && kf > 1) gload(1, a1, a1e);
     if (prio) __builtin_amdgcn_s_setprio(0);
+    STAMP(3);
     {  // the previous groups' completed blocks, while the loads are in flight
       const int fe = (int)((op + obal) & ~15u) - (int)obal;
       if (fe >= (int)flushed + 1024) flush_to((u32)fe);
     }
+    STAMP(4);
     const u32 wa = (u32)((int)t_op - sbase);
+#ifdef FSG_DBG_NOA  // diagnostic builds only (instruction accounting): wrong output
+    kf = 0;
+#endif
     if (kf > 0) or_store(sb, wa, shf(a0, a0e, reg0 ? 0u : sh), len < 16 ? len : 16u, mtab);
     if (m1) {
       if (kf > 1) or_store(sb, wa + 16, shf(a1, a1e, sh), len - 16 < 16 ? len - 16 : 16u, mtab);
@@ -1526,36 +1539,64 @@ __device__ __forceinline__ void exec5_message(
     }
     wave_lds_fence();
 
-    // ---------- rounds B: near chunks, in LDS, in dependency order
+    STAMP(5);
+    // ---------- rounds B: near chunks, in LDS, in dependency order.  Per
+    // lane: the current chunk's window offsets (cw destination, sw source),
+    // its length n and the end of the bytes it needs, ne (~0: lane done).
+    // A chunk runs once ne <= the first unfinished chunk's destination; it is
+    // written read-modify-write: 16 window bytes are read and written back
+    // with the chunk's n bytes merged in (v_bfi with the n-byte mask), so the
+    // write is exact whatever n.  Within one write instruction overlapping
+    // lanes land highest-lane-last (tools/probes/lds_overlap_probe.hip), and
+    // a lane's 16-byte span only reaches later chunks, whose bytes it writes
+    // back unchanged unless their own (higher) lane writes them.
     u32 rem = (fits && kf < nch) ? len - 16 * kf : 0u;
-    u32 cd = t_op + 16 * kf, cs = src + 16 * kf;
+    u32 cw = (u32)((int)t_op - sbase) + 16 * kf;
+    u32 sw = (u32)((int)src - sbase) + 16 * kf;
     const u32 stp = pat ? pat_step(off) : 16u;
     bool pf = pat;
+    u32 n = rem < stp ? rem : stp;
+    u32 ne = rem ? (pf ? cw : sw + n) : 0xffffffffu;
     u64 pend = __ballot(rem > 0);
+#ifdef FSG_DBG_NOB  // diagnostic builds only (instruction accounting): wrong output
+    pend = 0;
+#endif
     while (pend) {
-      const u32 W = readlane(cd, (u32)__builtin_ctzll(pend));
-      const u32 n = rem < stp ? rem : stp;
-      const u32 ne = pf ? cd : cs + n;
-      if (rem > 0 && ne <= W) {
-        u32x4 x = lds_read16(sb + ((int)cs - sbase));
+      const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
+      if (ne <= W) {
+        u32x4 x = lds_read16(sb + sw);
         if (pf) x = expand_pattern(x, off, sel_tab);
-        or_store(sb, (u32)((int)cd - sbase), x, n, mtab);
+        const u32x4 o = lds_read16(sb + cw);
+        const u32x4 mk = mtab[n];
+        u32x4 y;
+        y[0] = (x[0] & mk[0]) | (o[0] & ~mk[0]);
+        y[1] = (x[1] & mk[1]) | (o[1] & ~mk[1]);
+        y[2] = (x[2] & mk[2]) | (o[2] & ~mk[2]);
+        y[3] = (x[3] & mk[3]) | (o[3] & ~mk[3]);
+        __builtin_memcpy(sb + cw, &y, 16);
         rem -= n;
-        cd += n;
-        cs = pat ? cd - stp : cs + n;
+        cw += n;
+        sw = pat ? cw - stp : sw + n;
         pf = false;
+        n = rem < stp ? rem : stp;
+        ne = rem ? sw + n : 0xffffffffu;
       }
       wave_lds_fence();
       pend = __ballot(rem > 0);
     }
     op += tot_len;
     head += k_tags;
+    STAMP(6);
   }
   if (op != op1) {  // the stream ended early (snappy.cc:858-868)
     if (lane == 0) status[m] = kCorrupt;
     return;
   }
   flush_to(op1);
+#ifdef FSG_STAMPS
+  if (lane == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(&g_stamps[k], (unsigned long long)st_[k]);
+#endif
 }
 
 // 6 waves per SIMD (62 VGPRs, LDS 25 KB per block); 7 waves (smaller tag ring

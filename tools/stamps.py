@@ -19,8 +19,10 @@ import torch  # noqa: E402
 
 import fsg  # noqa: E402
 
-PHASES = ["fill", "decode+scan", "pieces+prefetch", "slide+pmap+gather", "roundA", "roundsB",
-          "flush", "longlit"]
+PHASES4 = ["fill", "decode+scan", "pieces+prefetch", "slide+pmap+gather", "roundA", "roundsB",
+           "flush", "longlit"]
+PHASES5 = ["fill", "decode", "scan+checks+slide+prefetch+zero", "classify+roundA loads", "flush",
+           "roundA stores", "roundsB", "longlit"]
 
 
 def main():
@@ -44,7 +46,9 @@ def main():
     d_out = torch.zeros(b.total, dtype=torch.uint8, device=dev)
     d_ol = torch.zeros(n, dtype=torch.int32, device=dev)
     dws = codec.decompress_workspace(n, ctot)
-    codec.select_kernels(4, 0)
+    variant = int(os.environ.get("FSG_STAMPS_VARIANT", "5"))
+    codec.select_kernels(variant, 0)
+    PHASES = PHASES5 if variant == 5 else PHASES4
     buf = (ctypes.c_ulonglong * 16)()
     codec.decompress(d_c, d_co, d_cl, n, d_out, d_ro, d_rl, d_ol, d_st, workspace=dws)
     torch.cuda.synchronize()
