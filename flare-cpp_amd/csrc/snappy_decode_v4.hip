@@ -767,9 +767,12 @@ namespace {
 #ifndef FSG_FAR_SC1
 #define FSG_FAR_SC1 1
 #endif
+// Window and kept history: 3 KiB / 1 KiB at 7 waves per SIMD (C3 6.35 ->
+// 6.20 ms against 4 KiB / 2 KiB at 6 waves, A/B on one box; 4 KiB / 1 KiB
+// at 6 waves 6.33, a 256-entry tag ring 7.04).
 #ifndef FSG_WINDOW
-#define FSG_WINDOW 4096
-#define FSG_KEEP 2048
+#define FSG_WINDOW 3072
+#define FSG_KEEP 1024
 #endif
 constexpr u32 kWindow = FSG_WINDOW;  // LDS output window per wave
 constexpr u32 kKeep = FSG_KEEP;      // history kept when the window slides
@@ -1354,10 +1357,10 @@ __device__ __forceinline__ void exec5_message(
     if (avail == 0 || op >= op1) break;
     const u32 take0 = avail < 64 ? avail : 64u;
     const bool valid = lane < take0;
-    const u32 pos = valid ? ring[(head + lane) & (kTagRing - 1)] : 0u;
-    if (pf_head != head || pf_cnt < take0) {
-      if (valid) prefetch(pos);
-    }
+    // every lane reads the ring and prefetches: a lane past the valid tags
+    // reads a stale position, whose buffer loads return message bytes or 0
+    const u32 pos = ring[(head + lane) & (kTagRing - 1)];
+    if (pf_head != head || pf_cnt < take0) prefetch(pos);
     if (prio) __builtin_amdgcn_s_setprio(1);
 
     // ---------- decode one tag per lane (checked by pass 1)
@@ -1436,7 +1439,7 @@ __device__ __forceinline__ void exec5_message(
     const u32 k_tags = (u32)__builtin_popcountll(__ballot(fits));
     const u32 tot_len = readlane(incl, k_tags - 1);
     // the writer's checks (snappy.cc:1166, :1200, :1400, :1410, :1466)
-    if (__any(fits && ((u64)t_op + len > op1 || (!is_lit && (off == 0 || off > t_op - op0))))) {
+    if (__any(fits && (len > op1 - t_op || (!is_lit && (off == 0 || off > t_op - op0))))) {
       if (lane == 0) status[m] = kCorrupt;
       return;
     }
@@ -1463,7 +1466,7 @@ __device__ __forceinline__ void exec5_message(
       const u32 nh = head + k_tags;
       const u32 na = tail - nh;
       const u32 ncnt = na < 64 ? na : 64u;
-      if (lane < ncnt) prefetch(ring[(nh + lane) & (kTagRing - 1)]);
+      prefetch(ring[(nh + lane) & (kTagRing - 1)]);
       pf_head = nh;
       pf_cnt = ncnt;
     }
@@ -1481,15 +1484,12 @@ __device__ __forceinline__ void exec5_message(
     const u32 src = is_lit ? lsrc : t_op - off;
     const u32 nch = (len + 15) >> 4;
     const bool pat = !is_lit && off < 16 && off < len;
-    u32 kf = 0;
-    if (fits) {
-      if (is_lit) {
-        kf = nch;
-      } else if (!pat && (int)src < sbase) {
-        const u32 kfar = (((u32)(sbase - (int)src) - 1) >> 4) + 1;
-        kf = kfar < nch ? kfar : nch;
-      }
-    }
+    // leading chunks done in round A: all of a literal's; a copy's whose
+    // 16-byte source starts below the window base (none for a pattern)
+    const u32 below = (u32)(sbase - (int)src);  // > 0 as int: far
+    const u32 kfar = (int)below > 0 ? ((below - 1) >> 4) + 1 : 0u;
+    const u32 kc = pat ? 0u : (kfar < nch ? kfar : nch);
+    const u32 kf = fits ? (is_lit ? nch : kc) : 0u;
     const bool reg0 = is_lit && nb == 0;
     // Loads only here: the data is first used after the flush below, so all
     // of a lane's chunk loads are in flight together.  A literal chunk is a
@@ -1522,9 +1522,6 @@ __device__ __forceinline__ void exec5_message(
     }
     STAMP(4);
     const u32 wa = (u32)((int)t_op - sbase);
-#ifdef FSG_DBG_NOA  // diagnostic builds only (instruction accounting): wrong output
-    kf = 0;
-#endif
     if (kf > 0) or_store(sb, wa, shf(a0, a0e, reg0 ? 0u : sh), len < 16 ? len : 16u, mtab);
     if (m1) {
       if (kf > 1) or_store(sb, wa + 16, shf(a1, a1e, sh), len - 16 < 16 ? len - 16 : 16u, mtab);
@@ -1605,8 +1602,11 @@ __device__ __forceinline__ void exec5_message(
 // device counter (blocks dispatch in order, so the longest messages start
 // first); every other block runs the wave-per-message mapping and skips them.
 // (A fully persistent grid was measured slower on uniform batches.)
+#ifndef FSG_EXEC_WAVES
+#define FSG_EXEC_WAVES 7
+#endif
 template <int V>
-__global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_per_eu(6, 6))) void exec_kernel(
+__global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_per_eu(FSG_EXEC_WAVES, FSG_EXEC_WAVES))) void exec_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, u8* out,
     const u64* __restrict__ out_off, const u32* __restrict__ out_len,
@@ -1615,14 +1615,12 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     const u32* __restrict__ seg_count, const u32* __restrict__ whole_list,
     const u32* __restrict__ whole_count, u32* __restrict__ exec_next, u32 big_blocks,
     u32 big_threshold, u32 prio, u32 keep_hist) {
-  // per wave: the tag ring, then the output window; a large message's index
-  // walk stages its input over both (kBigStageBytes + 16 <= their size)
+  // per wave: the tag ring, then the output window
   __shared__ __attribute__((aligned(16))) u8 wl_s[kWavesPerBlock][4 * kTagRing + kWindow + 32];
   __shared__ __attribute__((aligned(16))) u8 pmap_s[kWavesPerBlock][V == 5 ? 1 : kMaxPieces];
   __shared__ u32x4 sel_tab[16];
   __shared__ u32 tagtab[V == 5 ? 256 : 1];
   __shared__ u32x4 mask_tab[17];
-  static_assert(kBigStageBytes + 16 <= 4 * kTagRing + kWindow + 32, "stage fits the wave's LDS");
   static_assert(kWavesPerBlock * 64 == 256, "one tag table entry per thread");
 
   if (threadIdx.x < 64) init_pattern_table(sel_tab, threadIdx.x);

@@ -270,6 +270,9 @@ bool Device::run(const std::vector<Request*>& reqs, Kind kind, Counters* ctr) {
     return false;
   // D2H target: a pinned slab the outputs are adopted from, else staging
   OutSlab* slab = validate ? nullptr : AcquireOutSlab(total_out + 16);
+  // under slab pressure outputs are copied, so this slab returns to the pool
+  // right after the batch instead of being held by long-lived cord_bufs
+  const bool adopt = slab && !OutSlabsUnderPressure();
   if (!validate && slab == nullptr && !h_out.reserve(total_out + 16)) return false;
   uint8_t* hout = slab ? OutSlabData(slab) : h_out.as<uint8_t>();
 
@@ -350,7 +353,7 @@ bool Device::run(const std::vector<Request*>& reqs, Kind kind, Counters* ctr) {
       bytes_in += in_len[i];
       if (validate) continue;
       const uint32_t L = out_len[i];
-      if (slab && L >= kAdoptMin) {
+      if (adopt && L >= kAdoptMin) {
         OutSlabRef(slab);
         r->out->append_user_data(hout + out_off[i], L, AdoptedDeleter);
         ++adopted;

@@ -101,7 +101,7 @@ size_t g_out_total = 0;
 size_t out_cap_bytes() {
   static const size_t cap = [] {
     const char* e = getenv("FLARE_SNAPPY_GPU_PINNED_OUT_BYTES");
-    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)(16ull << 30);
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)(4ull << 30);
   }();
   return cap;
 }
@@ -154,6 +154,14 @@ OutSlab* AcquireOutSlab(size_t bytes) {
   }
   best->refs.store(1, std::memory_order_relaxed);
   return best;
+}
+
+bool OutSlabsUnderPressure() {
+  // more than half the cap allocated and no slab free: adopted outputs are
+  // holding the pool, so new outputs are copied and their slab returns to
+  // the pool right after the batch
+  std::lock_guard<std::mutex> lk(g_out_mu);
+  return g_out_free.empty() && 2 * g_out_total > out_cap_bytes();
 }
 
 uint8_t* OutSlabData(OutSlab* s) { return s->data; }

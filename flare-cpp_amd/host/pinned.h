@@ -12,8 +12,13 @@ namespace flare::gpu {
 // released it.
 struct OutSlab;
 // nullptr when the pool is at its cap (FLARE_SNAPPY_GPU_PINNED_OUT_BYTES,
-// default 16 GiB) or pinned memory is unavailable: the caller copies instead.
+// default 4 GiB) or pinned memory is unavailable: the caller copies instead.
+// An adopted output keeps its whole slab out of the pool until the last
+// cord_buf holding a piece of it dies.
 OutSlab* AcquireOutSlab(size_t bytes);  // holds one reference
+// True when over half the cap is allocated and no slab is free (adopted
+// outputs are holding the pool): callers copy outputs instead of adopting.
+bool OutSlabsUnderPressure();
 uint8_t* OutSlabData(OutSlab* s);
 void OutSlabRef(OutSlab* s);
 void OutSlabRelease(OutSlab* s);

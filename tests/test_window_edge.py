@@ -9,17 +9,17 @@ from window_edge import edge_stream, window_model
 
 
 def test_window_model_rules():
-    # 64 one-byte literals per group; the window slides once output passes 4096
+    # 64 16-byte literals per group; the window slides once output passes 3072
     tags = [(True, 16, 0)] * 400
     sb, pos = window_model(tags)
     assert pos[64] == 64 * 16 and sb[0] == 0
     first_slide = next(i for i, s in enumerate(sb) if s)
-    assert pos[first_slide] + 64 * 16 > 4096 >= pos[first_slide]
-    assert sb[first_slide] == (pos[first_slide] - 2048) & ~15
+    assert pos[first_slide] + 64 * 16 > 3072 >= pos[first_slide]
+    assert sb[first_slide] == (pos[first_slide] - 1024) & ~15
     # a long literal runs alone and restarts the window below its end
     sb, pos = window_model([(True, 10, 0), (True, 100, 0), (False, 8, 20)])
     assert sb[2] == ((110 & ~15) - 16)
-    # the first slide comes before the group that would pass 4096: one tag per
+    # the first slide comes before the group that would pass 3072: one tag per
     # lane cuts groups at 1,024 output bytes (51 x 20-byte literals), pieces
     # at 64 pieces (32 x two-piece literals)
     tags = [(True, 20, 0)] * 400
@@ -27,7 +27,7 @@ def test_window_model_rules():
         sb, pos = window_model(tags, rule)
         first_slide = next(i for i, s in enumerate(sb) if s)
         assert first_slide % per_group == 0, rule
-        assert pos[first_slide] + 20 * per_group > 4096 >= pos[first_slide], rule
+        assert pos[first_slide] + 20 * per_group > 3072 >= pos[first_slide], rule
 
 
 def test_edge_streams_valid():

@@ -2,7 +2,7 @@
 
 exec_message (flare-cpp_amd/csrc/snappy_decode_v4.hip, pass 2) assembles a
 message's output in a per-wave window holding output positions
-[sbase, sbase + 4096).  A copy whose source starts below sbase is a "far" copy:
+[sbase, sbase + 3072).  A copy whose source starts below sbase is a "far" copy:
 round A loads it from the output already stored to global memory; any other
 copy reads the window (rounds B).  `window_model` replays the kernel's group
 and window rules on a tag list:
@@ -17,7 +17,7 @@ and window rules on a tag list:
     block below the block holding the new write position:
     sbase = (op & ~15) - 16;
   * before a group whose output would overrun the window, the window slides to
-    sbase = (op - 2048) & ~15.
+    sbase = (op - 1024) & ~15.
 
 (Slots 16-byte aligned, as the test harness allocates them.)  The generator
 lays down the tag lengths first, runs the model, then gives each copy an
@@ -29,7 +29,7 @@ from __future__ import annotations
 
 import numpy as np
 
-WINDOW, KEEP, MAX_PIECES, GROUP_BYTES = 4096, 2048, 64, 1024
+WINDOW, KEEP, MAX_PIECES, GROUP_BYTES = 3072, 1024, 64, 1024
 
 
 def _pieces(ln: int, off: int) -> int:
