@@ -5,7 +5,7 @@
 # usage: bash tools/gpurun/r2.sh   (outputs under gpurun_out/r2/)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r2
+O=${OUT:-gpurun_out/r2}
 mkdir -p $O
 if [ -n "$PROBES" ]; then
   for p in $PROBES; do

@@ -6,7 +6,11 @@ The op under test may be several kernels (decode v4: index_kernel +
 exec_kernel + the fallback pass); the per-launch traffic is the sum over the
 op's kernels of each kernel's average over its dispatches.
 
-    python tools/pmc_summary.py WORKLOAD FETCH.csv WRITE.csv ALGO_BYTES [scale]
+    python tools/pmc_summary.py WORKLOAD FETCH.csv WRITE.csv ALGO_BYTES [PIPES_PER_OP]
+
+PIPES_PER_OP (compress only, default 1): encode_pipe_kernel launches per
+compress op -- 1 when no message is split (C3: 64 KiB bodies), 2 when the
+batch has split messages (the second is the fallback pass).
 
 FETCH_SIZE is corrected per kernel by its access pattern (MI355X_MICROARCH.md:
 FETCH_SIZE counts half the bytes of wide coalesced 16-B-per-lane reads):
@@ -48,6 +52,7 @@ def per_kernel(path, counter):
 
 def main():
     workload, fetch_csv, write_csv, algo = sys.argv[1:5]
+    pipes_per_op = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     op = "decompress" if workload.endswith("decompress") else "compress"
     names = OP_KERNELS[op]
     f = per_kernel(fetch_csv, "FETCH_SIZE")
@@ -59,8 +64,8 @@ def main():
             continue
         fa = sum(f.get(k, [0])) / max(1, len(f.get(k, [])))
         wa = sum(w.get(k, [0])) / max(1, len(w.get(k, [])))
-        # the fallback pass runs once per op; encode_pipe runs twice per compress op
-        mult = 2 if (op == "compress" and k.endswith("encode_pipe_kernel")) else 1
+        # per-dispatch averages: encode_pipe runs pipes_per_op times per compress op
+        mult = pipes_per_op if (op == "compress" and k.endswith("encode_pipe_kernel")) else 1
         scale = FETCH_SCALE.get(k.split("::")[-1], 1.0)
         out["kernels"][k] = {"fetch_kb": round(fa, 1), "write_kb": round(wa, 1), "fetch_scale": scale,
                              "dispatches": len(f.get(k, []))}
