@@ -54,6 +54,10 @@ constexpr int kIdxTagsOne = 32, kIdxTagsPlanned = 24;
 #ifndef FSG_IDX_ITER_CHECK
 #define FSG_IDX_ITER_CHECK 1
 #endif
+// Rounds B with pattern chunks outside the common path (see exec5_message).
+#ifndef FSG_ROUNDS_V2
+#define FSG_ROUNDS_V2 1
+#endif
 constexpr u32 kRingChunks = 16;              // 16-byte chunks per lane (256 B)
 constexpr u32 kRingDwords = kRingChunks * 4;
 constexpr u32 kAhead = 7;                    // chunks prefetched per iteration
@@ -1574,12 +1578,40 @@ __device__ __forceinline__ void exec5_message(
     u32 cw = (u32)((int)t_op - sbase) + 16 * kf;
     u32 sw = (u32)((int)src - sbase) + 16 * kf;
     const u32 stp = pat ? pat_step(off) : 16u;
-    bool pf = pat;
     u32 n = rem < stp ? rem : stp;
+    bool pf = pat;
     u32 ne = rem ? (pf ? cw : sw + n) : 0xffffffffu;
     u64 pend = __ballot(rem > 0);
 #ifdef FSG_DBG_NOB  // diagnostic builds only (instruction accounting): wrong output
     pend = 0;
+#endif
+#if FSG_ROUNDS_V2
+    // Most groups (~90% on text) hold no pattern copy: their rounds run a
+    // loop with no per-lane pattern state (the general loop below costs ~6
+    // more instructions per round).
+    if (!__ballot(pat && rem > 0)) {
+      while (pend) {
+        const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
+        if (ne <= W) {
+          const u32x4 x = lds_read16(sb + sw);
+          const u32x4 o = lds_read16(sb + cw);
+          const u32x4 mk = mtab[n];
+          u32x4 y;
+          y[0] = (x[0] & mk[0]) | (o[0] & ~mk[0]);
+          y[1] = (x[1] & mk[1]) | (o[1] & ~mk[1]);
+          y[2] = (x[2] & mk[2]) | (o[2] & ~mk[2]);
+          y[3] = (x[3] & mk[3]) | (o[3] & ~mk[3]);
+          __builtin_memcpy(sb + cw, &y, 16);
+          rem -= n;
+          cw += n;
+          sw += n;
+          n = rem < 16u ? rem : 16u;
+          ne = rem ? sw + n : 0xffffffffu;
+        }
+        wave_lds_fence();
+        pend = __ballot(rem > 0);
+      }
+    }
 #endif
     while (pend) {
       const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
