@@ -39,6 +39,7 @@
 #include "snappy_lane_decode.h"
 #include "snappy_pieces.h"
 
+#include <atomic>
 #include <mutex>
 
 namespace fsg {
@@ -308,20 +309,37 @@ __global__ __launch_bounds__(64) void index_plan_kernel(
 
 // kPlanned: index_plan_kernel ran first (statuses, bitmap bases and the
 // large-message list are in place; only kNeedLaneWalk messages are walked).
-template <bool kPlanned>
-__global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
+template <bool kPlanned, bool kLean = false>
+__global__ __launch_bounds__(64 * kIdxWaves)
+__attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, const u32* __restrict__ out_cap,
     u32* __restrict__ out_len, i32* __restrict__ status_out, u32 flags,
     u32* __restrict__ bm_counter, u32* __restrict__ bm_base_out,
     u32* __restrict__ bitmap, u64 bm_capacity_words, u32* __restrict__ big_count,
     u32* __restrict__ big_list, u32 big_threshold) {
-  constexpr int kIdxTags = kPlanned ? kIdxTagsPlanned : kIdxTagsOne;
+  // Lean geometry (the two-stream form, whose walk runs beside the previous
+  // batch's execution pass in the CU resources that pass leaves free: <= 80
+  // VGPRs, 12.3 KB of LDS): an 8-chunk input ring, 16 tags per iteration, 4
+  // chunks prefetched, 2 bit groups (an iteration's tags lie within the 128
+  // bytes the ring holds, so within 2 groups of 128 input bytes).
+  constexpr int kIdxTags = kLean ? 16 : (kPlanned ? kIdxTagsPlanned : kIdxTagsOne);
+  constexpr u32 kRC = kLean ? 8 : kRingChunks, kRD = kRC * 4, kAH = kLean ? 4 : kAhead;
+  constexpr u32 kBG = kLean ? 2 : 4, kBW = 4 * kBG;  // bit groups (4 words each) per lane
   // per wave, [dword][lane]; dword 64 = copy of dword 0; 65..68 absorb
   // unused prefetches
-  __shared__ u32 ring_s[kIdxWaves][(kRingDwords + 5) * kWave];
+  // The lean form takes its LDS dynamically (idx_lean_lds_bytes(), given at
+  // launch): with a compile-time size the compiler sizes the VGPR allocation
+  // for the occupancy that LDS alone would allow (97 registers reserved for
+  // 52 used), too many to fit beside the execution pass's waves.
+  extern __shared__ u32 idx_dyn_lds[];
+  __shared__ u32 ring_s[kLean ? 1 : kIdxWaves][kLean ? 1 : (kRD + 5) * kWave];
+  __shared__ u32 tagtab_s[kLean ? 1 : 256];
+  __shared__ u32 bmr_s[kLean ? 1 : kIdxWaves][kLean ? 1 : kBW * kWave];
   const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  u32* const ring = ring_s[wv];
+  u32* const ring = kLean ? idx_dyn_lds + wv * (kRD + 5) * kWave : ring_s[wv];
+  u32* const tagtab = kLean ? idx_dyn_lds + kIdxWaves * (kRD + 5) * kWave : tagtab_s;
+  u32* const bmr = kLean ? idx_dyn_lds + kIdxWaves * (kRD + 5) * kWave + 256 + wv * kBW * kWave : bmr_s[wv];
 
   const u32 lane = threadIdx.x & 63;
   // Tag table (the role of char_table, snappy.cc:516-549): per tag byte c,
@@ -329,7 +347,6 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
   // ((32 - 8 nb) & 31: a shift uses the low 5 bits of its operand), 5 long
   // literal, 8-15 advance without a long literal's length, 16-23 length
   // (short literal / copies).
-  __shared__ u32 tagtab[256];
 #pragma unroll
   for (u32 q = 0; q < 4 / kIdxWaves; ++q) {
     const u32 c = threadIdx.x * (4 / kIdxWaves) + q, type = c & 3, l0 = (c >> 2) + 1;
@@ -377,10 +394,10 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
 
   u32 wend = 0, iend = 0;
   auto ring_write = [&](u32 k, u32x4 v, bool live) {
-    const u32 d = live ? (k & (kRingChunks - 1)) * 4 : kRingDwords + 1;
+    const u32 d = live ? (k & (kRC - 1)) * 4 : kRD + 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) ring[(d + i) * kWave + lane] = v[i];
-    ring[(d == 0 ? kRingDwords : kRingDwords + 1) * kWave + lane] = v[0];
+    ring[(d == 0 ? kRD : kRD + 1) * kWave + lane] = v[0];
   };
   // Single-literal message (random bodies: the encoder emits one literal when
   // it finds no match): its first tag is a literal whose bytes end the input.
@@ -420,15 +437,13 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
   // is stored to the bitmap (if it holds bits) once the walk has left it.  One
   // iteration covers at most 3 groups (the input ring spans 256 bytes, and a
   // long literal that leaves it ends the lane's iteration).
-  __shared__ u32 bmr_s[kIdxWaves][16 * kWave];
-  u32* const bmr = bmr_s[wv];
 #pragma unroll
-  for (u32 q = 0; q < 16; ++q) bmr[q * kWave + lane] = 0;
+  for (u32 q = 0; q < kBW; ++q) bmr[q * kWave + lane] = 0;
   u32 fg = 0;  // lowest group that may still hold unstored bits
 
-  u32x4 g[kAhead];
+  u32x4 g[kAH];
 #pragma unroll
-  for (u32 c = 0; c < kAhead; ++c) g[c] = u32x4{0, 0, 0, 0};
+  for (u32 c = 0; c < kAH; ++c) g[c] = u32x4{0, 0, 0, 0};
   u32 gk_w = 0, gn_w = 0;
 
   __builtin_amdgcn_s_waitcnt(0);
@@ -447,7 +462,7 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
     // the compiler does not move LDS reads above the atomic.
     auto ring_read = [&](u32 at, u32& lo, u32& hi) {
       const u32 P = at + ibal;
-      const u32 dw = (P >> 2) & (kRingDwords - 1);
+      const u32 dw = (P >> 2) & (kRD - 1);
       lo = ring[dw * kWave + lane];
       hi = ring[(dw + 1) * kWave + lane];
     };
@@ -493,7 +508,7 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
       // The bit and length of such a tag land only in state that a corrupt
       // message never stores.
       lmax = look && lpart > lmax ? lpart : lmax;
-      atomicOr(&bmr[((ip >> 5) & 15) * kWave + lane], look ? 1u << (ip & 31) : 0u);
+      atomicOr(&bmr[((ip >> 5) & (kBW - 1)) * kWave + lane], look ? 1u << (ip & 31) : 0u);
 #else
       // Tag bytes and literal bytes present (:744-761): the step fits the
       // bytes left (ip < n_in whenever `look`).  A 4-byte literal length can
@@ -508,7 +523,7 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
       // unconditional (bits land in the LDS ring even without a bitmap): a
       // per-tag branch here would split the unrolled walk into one basic
       // block per tag
-      atomicOr(&bmr[((ip >> 5) & 15) * kWave + lane], take ? 1u << (ip & 31) : 0u);
+      atomicOr(&bmr[((ip >> 5) & (kBW - 1)) * kWave + lane], take ? 1u << (ip & 31) : 0u);
 #endif
       op += look ? len : 0u;
       ip = ip_next;
@@ -526,10 +541,10 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
     if (bm) {
       const u32 cur = status < 0 ? ip >> 7 : 0xffffffffu;
 #pragma unroll
-      for (u32 k = 0; k < 4; ++k) {
+      for (u32 k = 0; k < kBG; ++k) {
         const u32 gi = fg + k;
         if (gi < cur) {
-          const u32 sl = (gi & 3) * 4;
+          const u32 sl = (gi & (kBG - 1)) * 4;
           u32x4 v;
 #pragma unroll
           for (u32 q = 0; q < 4; ++q) v[q] = bmr[(sl + q) * kWave + lane];
@@ -540,12 +555,12 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
           }
         }
       }
-      fg = cur > fg + 4 ? cur : (cur > fg ? cur : fg);
+      fg = cur > fg + kBG ? cur : (cur > fg ? cur : fg);
     }
 
     // ---------- land the chunks loaded last iteration
 #pragma unroll
-    for (u32 c = 0; c < kAhead; ++c) ring_write(gk_w + c, g[c], c < gn_w);
+    for (u32 c = 0; c < kAH; ++c) ring_write(gk_w + c, g[c], c < gn_w);
     wend = gn_w ? gk_w + gn_w : wend;
 
     // ---------- prefetch from the parse position
@@ -555,9 +570,9 @@ __global__ __launch_bounds__(64 * kIdxWaves) void index_kernel(
       const u32 base = pc >= iend ? pc : iend;  // a long literal jumped past the ring: restart
       u32 cnt = 0;
 #pragma unroll
-      for (u32 c = 0; c < kAhead; ++c) {
+      for (u32 c = 0; c < kAH; ++c) {
         const u32 k = base + c;
-        const bool ok = status < 0 && k <= last_chunk && k <= pc + (kRingChunks - 1);
+        const bool ok = status < 0 && k <= last_chunk && k <= pc + (kRC - 1);
         cnt += ok ? 1u : 0u;
         const u32 kk = k <= last_chunk ? k : last_chunk;
         g[c] = *reinterpret_cast<const u32x4*>(n_in ? abase + 16 * kk
@@ -1804,6 +1819,10 @@ static SideStream* side_stream() {
   return s->stream ? s : nullptr;
 }
 
+// Dynamic LDS of the lean lane walk: per wave an 8-chunk input ring (+5
+// dwords) and 2 bit groups, [dword][lane]; the 256-entry tag table.
+constexpr size_t idx_lean_lds_bytes() { return 4 * (kIdxWaves * (8 * 4 + 5 + 8) * kWave + 256); }
+
 hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u8* out, const u64* out_off,
                             const u32* out_cap, u32* out_len, i32* status,
@@ -1819,6 +1838,15 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     if (!two) return hipErrorNotReady;
   }
   hipStream_t const caller_stream = stream;
+  // Two-stream form: the lean lane walk (FSG_LEAN_WALK=0: the standard one).
+  // Measured (C3, stream of two alternating batches, one box): lean 6.13 ms
+  // per batch, standard 6.57, serial 6.15; an execution pass made persistent
+  // at 5 or 6 blocks per CU to leave wave slots for the walk: 6.38 / 7.25
+  // (the dispatcher does not spread a persistent grid evenly).
+  static const bool kLeanWalk = [] {
+    const char* e = getenv("FSG_LEAN_WALK");
+    return !(e && e[0] == '0');
+  }();
   if (two) stream = pass1_stream;  // every pass-1 launch below goes there
   // pass 2: one tag per lane (5) or <= 16-byte pieces per lane (4)
   auto* const ek = exec_variant == 4 ? &exec_kernel<4> : &exec_kernel<5>;
@@ -1853,6 +1881,10 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   auto launch_index = [&](bool planned) -> hipError_t {
     if (planned)
       index_kernel<true><<<idx_blocks, 64 * kIdxWaves, 0, stream>>>(
+          in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
+          cap_words, big_count, big_list, big_threshold);
+    else if (two && kLeanWalk)
+      index_kernel<false, true><<<idx_blocks, 64 * kIdxWaves, idx_lean_lds_bytes(), stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
           cap_words, big_count, big_list, big_threshold);
     else
