@@ -1842,7 +1842,10 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   // Measured (C3, stream of two alternating batches, one box): lean 6.13 ms
   // per batch, standard 6.57, serial 6.15; an execution pass made persistent
   // at 5 or 6 blocks per CU to leave wave slots for the walk: 6.38 / 7.25
-  // (the dispatcher does not spread a persistent grid evenly).
+  // (the dispatcher does not spread a persistent grid evenly); the execution
+  // pass held to six blocks per CU by padding its LDS, with a two-wave lean
+  // walk in the space left: 6.32 vs serial 6.11 (the walk's instructions
+  // compete with an execution pass already at the issue limit).
   static const bool kLeanWalk = [] {
     const char* e = getenv("FSG_LEAN_WALK");
     return !(e && e[0] == '0');
@@ -1935,15 +1938,24 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
         reinterpret_cast<u32*>(w + 160), whole_list, reinterpret_cast<u32*>(w + 224));
     return hipGetLastError();
   };
+  // The forked path's large-message launch runs alone once the lane walk's
+  // side finishes, so it takes a full machine of blocks (7 per CU): CM 9.9 ->
+  // 8.85 ms against 512 blocks (A/B on one box, twice; 4096: 8.86).
+  static const u32 kBigBlocksFork = [] {
+    const char* e = getenv("FSG_EXEC_BIG_BLOCKS");
+    const int v = e ? atoi(e) : 1792;
+    return v >= 1 ? (u32)v : 1792u;
+  }();
   auto launch_big = [&](hipStream_t st) -> hipError_t {
     hipError_t e2 = launch_index_big(st);
     if (e2 != hipSuccess) return e2;
     // the large-message blocks only (exit after one atomic when the lists
     // are empty)
-    ek<<<big_blocks, kWavesPerBlock * 64, 0, st>>>(
+    const u32 fork_big_blocks = small_blocks < kBigBlocksFork ? small_blocks : kBigBlocksFork;
+    ek<<<fork_big_blocks, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
-        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), big_blocks, big_threshold, 0u,
+        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), fork_big_blocks, big_threshold, 0u,
         keep_hist);
     return hipGetLastError();
   };
