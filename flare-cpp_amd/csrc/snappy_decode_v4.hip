@@ -55,6 +55,10 @@ constexpr int kIdxTagsOne = 32, kIdxTagsPlanned = 24;
 #ifndef FSG_IDX_ITER_CHECK
 #define FSG_IDX_ITER_CHECK 1
 #endif
+// Pass 1b walks two 64-byte windows per step (see index_big_message).
+#ifndef FSG_BIG_TWO_WINDOWS
+#define FSG_BIG_TWO_WINDOWS 1
+#endif
 // Rounds B with pattern chunks outside the common path (see exec5_message).
 #ifndef FSG_ROUNDS_V2
 #define FSG_ROUNDS_V2 1
@@ -623,6 +627,139 @@ __device__ __forceinline__ i32 index_big_message(
   int spos = -1;  // message position of stage byte 0 (-1: nothing staged)
   u32 send = 0;   // positions [spos, send) are valid in the stage
 
+#if FSG_BIG_TWO_WINDOWS
+  // Two 64-byte windows per step, A = [wb, wb + 64) and B = [wb + 64,
+  // wb + 128), each lane decoding one candidate tag in each: the pointer
+  // doubling does not depend on where the chain enters a window, so both
+  // windows' doublings run interleaved (one latency chain of shuffles per
+  // 128 bytes instead of per 64), and B's chain is read at A's exit.
+  while (status < 0) {
+    if (ip >= n_in) {  // end of input between tags (snappy.cc:858-868)
+      status = (ip == n_in && op == expected) ? kOk : kCorrupt;
+      break;
+    }
+    const u32 wb = ip & ~31u;
+    // ---------- stage input covering [wb, wb + 128 + 8)
+    if (spos < 0 || wb < (u32)spos || wb + 136 > send) {
+      const u32 c0 = (wb + ibal) >> 4;
+      u32x4 x[kBigStageChunks / 64];
+#pragma unroll
+      for (u32 r = 0; r < kBigStageChunks / 64; ++r) {
+        u32 k = c0 + r * 64 + lane;
+        k = k <= last_chunk ? k : last_chunk;
+        x[r] = *reinterpret_cast<const u32x4*>(abase + 16 * k);
+      }
+      wave_lds_fence();  // previous window's stage reads are done
+#pragma unroll
+      for (u32 r = 0; r < kBigStageChunks / 64; ++r)
+        *reinterpret_cast<u32x4*>(st + 4 * (r * 64 + lane)) = x[r];
+      wave_lds_fence();
+      spos = (int)(16 * c0) - (int)ibal;
+      send = (u32)spos + kBigStageBytes - 8;
+    }
+    // ---------- every lane decodes the tag that would start at wb + lane
+    // (A) and at wb + 64 + lane (B): length, offset, next position, local
+    // validity (tag and literal bytes present), successor lane in the window
+    struct Cand {
+      u32 len, coff, nxt, J;
+      bool lit, bad_local;
+    };
+    auto decode = [&](u32 p) {
+      const u32 s = p - (u32)spos;
+      const u32 dw = s >> 2, bsh = s & 3;
+      const u32 lo = st[dw], hi = st[dw + 1];
+      const u32 t0 = alignbyte(hi, lo, bsh);
+      const u32 b4 = (hi >> (8 * bsh)) & 0xffu;
+      const u32 c = t0 & 0xffu;
+      const u32 type = c & 3;
+      Cand d;
+      d.lit = type == 0;
+      const u32 l0 = (c >> 2) + 1;
+      const bool longlit = d.lit & (l0 >= 61);
+      const u32 nb = d.lit ? (longlit ? l0 - 60 : 0u) : (1u << (type - 1));
+      const u32 ext = (b4 << 24) | (t0 >> 8);
+      const u32 val = nb >= 4 ? ext : ext & ((1u << (8 * nb)) - 1u);
+      d.len = d.lit ? (longlit ? val + 1u : l0) : (type == 1 ? 4 + ((c >> 2) & 7) : l0);
+      d.coff = type == 1 ? (((c >> 5) << 8) | val) : val;
+      const u32 avail = n_in - p - 1;
+      d.bad_local = (p >= n_in) | (avail < nb) | (d.lit & (avail - nb < d.len));
+      const u32 adv = 1 + nb + (d.lit ? d.len : 0u);
+      d.nxt = p + adv;
+      d.J = (d.bad_local || adv >= 64 - lane || d.nxt >= n_in) ? 64u : lane + adv;
+      return d;
+    };
+    const u32 pA = wb + lane, pB = wb + 64 + lane;
+    const Cand A = decode(pA), B = decode(pB);
+    // ---------- pointer doubling in both windows (see the one-window form)
+    u64 MA = 1ull << lane, MB = 1ull << lane;
+    u32 JA = A.J, JB = B.J;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const u32 sA = JA < 64 ? JA : lane, sB = JB < 64 ? JB : lane;
+      const u64 MAj = ((u64)(u32)__shfl((int)(u32)(MA >> 32), (int)sA, 64) << 32) |
+                      (u32)__shfl((int)(u32)MA, (int)sA, 64);
+      const u64 MBj = ((u64)(u32)__shfl((int)(u32)(MB >> 32), (int)sB, 64) << 32) |
+                      (u32)__shfl((int)(u32)MB, (int)sB, 64);
+      const u32 JAj = (u32)__shfl((int)JA, (int)sA, 64);
+      const u32 JBj = (u32)__shfl((int)JB, (int)sB, 64);
+      if (JA < 64) {
+        MA |= MAj;
+        JA = JAj;
+      }
+      if (JB < 64) {
+        MB |= MBj;
+        JB = JBj;
+      }
+    }
+    const u32 firstA = ip - wb;
+    const u64 SA = ((u64)readlane((u32)(MA >> 32), firstA) << 32) | readlane((u32)MA, firstA);
+    const u32 lastA = 63u - (u32)__builtin_clzll(SA);
+    const u32 ipA = readlane(A.nxt, lastA);  // where the chain leaves A
+    // B is entered when A's last tag is good and ends inside B
+    const bool enterB = ipA >= wb + 64 && ipA < wb + 128 && ipA < n_in;
+    const u32 firstB = enterB ? ipA - wb - 64 : 0u;
+    const u64 SB = enterB ? ((u64)readlane((u32)(MB >> 32), firstB) << 32) | readlane((u32)MB, firstB) : 0ull;
+    const bool inA = (SA >> lane) & 1ull, inB = (SB >> lane) & 1ull;
+    // output positions: A's chain from op, then B's
+    const u32 lvA = inA ? A.len : 0u;
+    const u32 incA = dpp_incl_scan(lvA);
+    const u32 t_opA = op + incA - lvA;
+    const u32 opA = op + readlane(incA, 63);
+    const u32 lvB = inB ? B.len : 0u;
+    const u32 incB = dpp_incl_scan(lvB);
+    const u32 t_opB = opA + incB - lvB;
+    // writer space and copy offset checks (:761, :1166, :1200, :1410, :1466)
+    const bool badA = inA && (A.bad_local || expected - t_opA < A.len || (!A.lit && A.coff - 1u >= t_opA));
+    const bool badB = inB && (B.bad_local || expected - t_opB < B.len || (!B.lit && B.coff - 1u >= t_opB));
+    if (__any(badA || badB)) {
+      status = kCorrupt;
+      break;
+    }
+    // 64 KiB output segments (see the one-window form)
+    if (seg) {
+      const bool spanA = inA && A.len > 0 && ((t_opA ^ (t_opA + A.len - 1)) >> 16) != 0;
+      const bool spanB = inB && B.len > 0 && ((t_opB ^ (t_opB + B.len - 1)) >> 16) != 0;
+      const bool xA = inA && !A.lit && t_opA - A.coff < (t_opA & ~0xffffu);
+      const bool xB = inB && !B.lit && t_opB - B.coff < (t_opB & ~0xffffu);
+      if (__any(spanA || spanB || xA || xB)) seg = false;
+      if (seg && inA && t_opA != 0 && (t_opA & 0xffffu) == 0 && t_opA + 4 <= expected)
+        __builtin_memcpy(ob + t_opA, &pA, 4);
+      if (seg && inB && t_opB != 0 && (t_opB & 0xffffu) == 0 && t_opB + 4 <= expected)
+        __builtin_memcpy(ob + t_opB, &pB, 4);
+    }
+    if (SB) {
+      const u32 lastB = 63u - (u32)__builtin_clzll(SB);
+      ip = readlane(B.nxt, lastB);
+      op = opA + readlane(incB, 63);
+    } else {
+      ip = ipA;
+      op = opA;
+    }
+    const u64 Sw = lane < 2 ? SA : SB;
+    const u32 wbits = (lane & 1) == 0 ? (u32)Sw : (u32)(Sw >> 32);
+    if (lane < 4 && wbits) bm[(wb >> 5) + lane] = wbits;
+  }
+#else
   while (status < 0) {
     if (ip >= n_in) {  // end of input between tags (snappy.cc:858-868)
       status = (ip == n_in && op == expected) ? kOk : kCorrupt;
@@ -719,6 +856,7 @@ __device__ __forceinline__ i32 index_big_message(
     const u32 wbits = lane == 0 ? (u32)S : (u32)(S >> 32);
     if (lane < 2 && wbits) bm[(wb >> 5) + lane] = wbits;
   }
+#endif
   return status;
 }
 
