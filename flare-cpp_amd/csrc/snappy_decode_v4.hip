@@ -288,6 +288,13 @@ __device__ __forceinline__ i32 index_prologue(
   return status;
 }
 
+// Size classes of the planned lane walk (see index_plan_kernel).
+constexpr u32 kWalkClasses = 16;
+__device__ __forceinline__ u32 walk_class(u32 n_in) {
+  const u32 lg = 31u - (u32)__builtin_clz(n_in | 1u);
+  return kWalkClasses - 1 - (lg < kWalkClasses - 1 ? lg : kWalkClasses - 1);
+}
+
 // Pass 1 plan (batches whose large messages are indexed on a side stream):
 // the prologue alone, so pass 1b can start on the listed large messages while
 // the lane walk (index_kernel<true>) runs; lanes left for the walk get
@@ -298,7 +305,8 @@ __global__ __launch_bounds__(64) void index_plan_kernel(
     u32* __restrict__ out_len, i32* __restrict__ status_out, u32 flags,
     u32* __restrict__ bm_counter, u32* __restrict__ bm_base_out,
     u32* __restrict__ bitmap, u64 bm_capacity_words, u32* __restrict__ big_count,
-    u32* __restrict__ big_list, u32 big_threshold) {
+    u32* __restrict__ big_list, u32 big_threshold, u32* __restrict__ walk_rank,
+    u32* __restrict__ walk_hist) {
   const u32 lane = threadIdx.x & 63;
   const u32 m = blockIdx.x * 64 + lane;
   const bool valid_msg = m < n_msgs;
@@ -309,6 +317,43 @@ __global__ __launch_bounds__(64) void index_plan_kernel(
                                 bm_counter, bm_base_out, bitmap, bm_capacity_words, big_count,
                                 big_list, big_threshold, &ip, &expected, &bm_base);
   if (valid_msg) status_out[m] = st < 0 ? kNeedLaneWalk : st;
+  if (!walk_rank) return;
+  // Size classes for the lane walk (a wave's walk lasts as long as its
+  // longest message): class = 15 - floor(log2(compressed size)), so the
+  // largest come first; rank within the class from a per-class counter.
+  const bool walk = valid_msg && st < 0;
+  const u32 cls = walk_class(n_in);
+  u32 mine = 0, below_mask_cnt = 0;
+#pragma unroll
+  for (u32 c = 0; c < kWalkClasses; ++c) {
+    const u64 b = __ballot(walk && cls == c);
+    const u32 cnt = (u32)__builtin_popcountll(b);
+    if (lane == c) mine = cnt;
+    if (cls == c) below_mask_cnt = (u32)__builtin_popcountll(b & ((1ull << lane) - 1));
+  }
+  u32 base = 0;
+  if (lane < kWalkClasses && mine) base = atomicAdd(&walk_hist[lane], mine);
+  base = (u32)__shfl((int)base, (int)(cls & (kWalkClasses - 1)), 64);
+  if (walk) walk_rank[m] = base + below_mask_cnt;
+}
+
+// Class offsets of the size-ordered lane walk (one block): exclusive prefix
+// of the per-class counts, and the number of messages to walk.
+__global__ __launch_bounds__(64) void walk_offsets_kernel(u32* __restrict__ walk_hist) {
+  const u32 lane = threadIdx.x;
+  const u32 v = lane < kWalkClasses ? walk_hist[lane] : 0u;
+  const u32 inc = wave_incl_scan(v);
+  if (lane < kWalkClasses) walk_hist[kWalkClasses + lane] = inc - v;
+  if (lane == 63) walk_hist[2 * kWalkClasses] = inc;
+}
+
+// Lane-walk order: perm[offset(class) + rank] = m for every message to walk.
+__global__ __launch_bounds__(256) void walk_scatter_kernel(
+    const u32* __restrict__ in_len, u32 n_msgs, const i32* __restrict__ status,
+    const u32* __restrict__ walk_rank, const u32* __restrict__ walk_hist, u32* __restrict__ perm) {
+  const u32 m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n_msgs || status[m] != kNeedLaneWalk) return;
+  perm[walk_hist[kWalkClasses + walk_class(in_len[m])] + walk_rank[m]] = m;
 }
 
 // kPlanned: index_plan_kernel ran first (statuses, bitmap bases and the
@@ -321,7 +366,8 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     u32* __restrict__ out_len, i32* __restrict__ status_out, u32 flags,
     u32* __restrict__ bm_counter, u32* __restrict__ bm_base_out,
     u32* __restrict__ bitmap, u64 bm_capacity_words, u32* __restrict__ big_count,
-    u32* __restrict__ big_list, u32 big_threshold) {
+    u32* __restrict__ big_list, u32 big_threshold, const u32* __restrict__ walk_perm,
+    const u32* __restrict__ walk_hist) {
   // Lean geometry (the two-stream form, whose walk runs beside the previous
   // batch's execution pass in the CU resources that pass leaves free: <= 80
   // VGPRs, 12.3 KB of LDS): an 8-chunk input ring, 16 tags per iteration, 4
@@ -371,8 +417,13 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     tagtab[c] = ((32 - 8 * nb) & 31) | (ll << 5) | (adv << 8) | (len << 16);
   }
   __syncthreads();
-  const u32 m = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid_msg = m < n_msgs;
+  // planned with a walk order: lane g walks message walk_perm[g], the
+  // messages grouped by size class so a wave's lanes finish together
+  const u32 gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ordered = kPlanned && walk_perm;
+  const u32 n_walk = ordered ? walk_hist[2 * kWalkClasses] : n_msgs;
+  const bool valid_msg = gid < n_walk;
+  const u32 m = ordered ? (valid_msg ? walk_perm[gid] : 0u) : gid;
 
   const u8* ib = valid_msg ? in + in_off[m] : in;
   const u32 n_in = valid_msg ? in_len[m] : 0u;
@@ -1923,7 +1974,7 @@ __global__ __launch_bounds__(64) void fallback_kernel(
 // count at 64, huge-message count at 96, queue heads at 128 and 192, segment
 // count at 160, whole-message count at 224) | bm_base[n] | big_list[n] |
 // seg_list[n] (u64) | whole_list[n] | bitmap words.
-constexpr u64 kListBases = 5;  // u32 arrays of n entries before the bitmap
+constexpr u64 kListBases = 8;  // u32 arrays of n entries before the bitmap
 size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
   const u64 words = total_in_bytes / 32 + 4ull * n_msgs + 64;
@@ -1976,6 +2027,11 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     if (!two) return hipErrorNotReady;
   }
   hipStream_t const caller_stream = stream;
+  // planned lane walk in size-class order (FSG_WALK_ORDER=0 disables)
+  static const bool kWalkOrder = [] {
+    const char* e = getenv("FSG_WALK_ORDER");
+    return !(e && e[0] == '0');
+  }();
   // Two-stream form: the lean lane walk (FSG_LEAN_WALK=0: the standard one).
   // Measured (C3, stream of two alternating batches, one box): lean 6.13 ms
   // per batch, standard 6.57, serial 6.15; an execution pass made persistent
@@ -2000,6 +2056,11 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   u32* big_list = reinterpret_cast<u32*>(w + 256 + base_bytes);
   u64* seg_list = reinterpret_cast<u64*>(w + 256 + 2 * base_bytes);
   u32* whole_list = reinterpret_cast<u32*>(w + 256 + 4 * base_bytes);
+  // the planned lane walk's order: ranks, the permutation, class counts and
+  // offsets (+ the walk count)
+  u32* walk_rank = reinterpret_cast<u32*>(w + 256 + 5 * base_bytes);
+  u32* walk_perm = reinterpret_cast<u32*>(w + 256 + 6 * base_bytes);
+  u32* walk_hist = reinterpret_cast<u32*>(w + 256 + 7 * base_bytes);
   u32* bitmap = reinterpret_cast<u32*>(w + 256 + kListBases * base_bytes);
   u64 cap_words = (ws_bytes - 256 - kListBases * base_bytes) / 4;
   if (cap_words >= kSingleLiteral) cap_words = kSingleLiteral - 1;  // bases < 2^31 words
@@ -2023,15 +2084,15 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     if (planned)
       index_kernel<true><<<idx_blocks, 64 * kIdxWaves, 0, stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
-          cap_words, big_count, big_list, big_threshold);
+          cap_words, big_count, big_list, big_threshold, kWalkOrder ? walk_perm : nullptr, walk_hist);
     else if (two && kLeanWalk)
       index_kernel<false, true><<<idx_blocks, 64 * kIdxWaves, idx_lean_lds_bytes(), stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
-          cap_words, big_count, big_list, big_threshold);
+          cap_words, big_count, big_list, big_threshold, nullptr, nullptr);
     else
       index_kernel<false><<<idx_blocks, 64 * kIdxWaves, 0, stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
-          cap_words, big_count, big_list, big_threshold);
+          cap_words, big_count, big_list, big_threshold, nullptr, nullptr);
     return hipGetLastError();
   };
   // Pass 1b and the large-message exec blocks run on a side stream, after a
@@ -2113,8 +2174,14 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     // the lane walk runs
     index_plan_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(
         in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
-        cap_words, big_count, big_list, big_threshold);
+        cap_words, big_count, big_list, big_threshold, kWalkOrder ? walk_rank : nullptr, walk_hist);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (kWalkOrder) {
+      walk_offsets_kernel<<<1, 64, 0, stream>>>(walk_hist);
+      walk_scatter_kernel<<<(n_msgs + 255) / 256, 256, 0, stream>>>(in_len, n_msgs, status, walk_rank,
+                                                                  walk_hist, walk_perm);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     std::lock_guard<std::mutex> lk(side->mu);
     if ((e = hipEventRecord(side->fork, stream)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(side->stream, side->fork, 0)) != hipSuccess) return e;
