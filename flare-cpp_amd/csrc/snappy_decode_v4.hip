@@ -922,13 +922,17 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
     u32* __restrict__ bitmap, const u32* __restrict__ big_count,
     const u32* __restrict__ big_list, u32* __restrict__ big_next, u32 n_msgs, u8* out,
     const u64* __restrict__ out_off, u64* __restrict__ seg_list, u32* __restrict__ seg_count,
-    u32* __restrict__ whole_list, u32* __restrict__ whole_count) {
+    u32* __restrict__ whole_list, u32* __restrict__ whole_count, u32 mode) {
   __shared__ u32 stage_s[4][kBigStageBytes / 4 + 4];
   const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const u32 lane = threadIdx.x & 63;
   const bool strict = flags & 2u;
-  const u32 n_huge = big_count[8];
-  const u32 count = big_count[0] + n_huge;
+  // mode 0: every listed message, the huge ones (> kHugeIndexBytes) first;
+  // 1: the huge ones only; 2: the others only (the forked path walks the two
+  // sets on two streams, so the others' execution starts without waiting for
+  // the longest walks)
+  const u32 n_huge = mode == 2 ? 0u : big_count[8];
+  const u32 count = (mode == 1 ? 0u : big_count[0]) + n_huge;
   if (count == 0) return;  // uniform batches: no atomics on the shared counter
   for (;;) {  // all-lane atomic: lane 0 adds 1, lane 0's result is the index
     const u32 got = atomicAdd(big_next, lane == 0 ? 1u : 0u);
@@ -1974,7 +1978,7 @@ __global__ __launch_bounds__(64) void fallback_kernel(
 // count at 64, huge-message count at 96, queue heads at 128 and 192, segment
 // count at 160, whole-message count at 224) | bm_base[n] | big_list[n] |
 // seg_list[n] (u64) | whole_list[n] | bitmap words.
-constexpr u64 kListBases = 8;  // u32 arrays of n entries before the bitmap
+constexpr u64 kListBases = 11;  // u32 arrays of n entries before the bitmap
 size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
   const u64 words = total_in_bytes / 32 + 4ull * n_msgs + 64;
@@ -1987,6 +1991,8 @@ size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
 // passes then run in one stream.
 struct SideStream {
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // the huge messages' pass 1b + execution (nullptr: not created)
+  hipEvent_t join2 = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   hipEvent_t pass1 = nullptr;  // two-stream calls: pass 1 done (fsg_decompress_batch_2s)
   std::mutex mu;
@@ -2004,6 +2010,10 @@ static SideStream* side_stream() {
         hipEventCreateWithFlags(&s->join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&s->pass1, hipEventDisableTiming) != hipSuccess)
       s->stream = nullptr;
+    // optional second side stream (the huge messages of a forked batch)
+    if (s->stream && (hipStreamCreateWithFlags(&s->stream2, hipStreamNonBlocking) != hipSuccess ||
+                      hipEventCreateWithFlags(&s->join2, hipEventDisableTiming) != hipSuccess))
+      s->stream2 = nullptr;
   });
   return s->stream ? s : nullptr;
 }
@@ -2028,6 +2038,10 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   }
   hipStream_t const caller_stream = stream;
   // planned lane walk in size-class order (FSG_WALK_ORDER=0 disables)
+  static const bool kSplitHuge = [] {  // FSG_SPLIT_HUGE=0: one side stream
+    const char* e = getenv("FSG_SPLIT_HUGE");
+    return !(e && e[0] == '0');
+  }();
   static const bool kWalkOrder = [] {
     const char* e = getenv("FSG_WALK_ORDER");
     return !(e && e[0] == '0');
@@ -2061,6 +2075,9 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   u32* walk_rank = reinterpret_cast<u32*>(w + 256 + 5 * base_bytes);
   u32* walk_perm = reinterpret_cast<u32*>(w + 256 + 6 * base_bytes);
   u32* walk_hist = reinterpret_cast<u32*>(w + 256 + 7 * base_bytes);
+  // the huge messages' pass-2 work lists (forked path, second side stream)
+  u64* seg_list2 = reinterpret_cast<u64*>(w + 256 + 8 * base_bytes);
+  u32* whole_list2 = reinterpret_cast<u32*>(w + 256 + 10 * base_bytes);
   u32* bitmap = reinterpret_cast<u32*>(w + 256 + kListBases * base_bytes);
   u64 cap_words = (ws_bytes - 256 - kListBases * base_bytes) / 4;
   if (cap_words >= kSingleLiteral) cap_words = kSingleLiteral - 1;  // bases < 2^31 words
@@ -2126,17 +2143,28 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   const char* fork_env = getenv("FSG_DECODE_FORK");  // read per call: tests set it
   const bool fork = !two && (fork_env ? atoi(fork_env) != 0 : n_msgs > 131072u);
   const u32 big_blocks = small_blocks < kBigBlocks ? small_blocks : kBigBlocks;
-  auto launch_index_big = [&](hipStream_t st) -> hipError_t {
-    // pass 1b: large messages, one wave each (an empty list costs one short
-    // launch); they land in pass 2's work lists
+  // pass 1b: large messages, one wave each (an empty list costs one short
+  // launch); they land in pass 2's work lists.  set 0: every large message
+  // (one stream) or the non-huge ones (forked); set 1: the huge ones (forked,
+  // second side stream), with their own counters and lists.
+  struct BigSet {
+    u32 *big_next, *seg_count, *whole_count, *exec_next;
+    u64* seg_list;
+    u32* whole_list;
+  };
+  const BigSet set0{reinterpret_cast<u32*>(w + 128), reinterpret_cast<u32*>(w + 160),
+                    reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), seg_list, whole_list};
+  const BigSet set1{reinterpret_cast<u32*>(w + 16), reinterpret_cast<u32*>(w + 32),
+                    reinterpret_cast<u32*>(w + 48), reinterpret_cast<u32*>(w + 240), seg_list2, whole_list2};
+  auto launch_index_big_set = [&](hipStream_t st, const BigSet& b, u32 mode) -> hipError_t {
     const u32 q = (n_msgs + 3) / 4;
     const u32 blocks = q < 1024u ? q : 1024u;
     index_big_kernel<<<blocks, 256, 0, st>>>(
         in, in_off, in_len, out_len, flags, status, bm_base, bitmap, big_count, big_list,
-        reinterpret_cast<u32*>(w + 128), n_msgs, out, out_off, seg_list,
-        reinterpret_cast<u32*>(w + 160), whole_list, reinterpret_cast<u32*>(w + 224));
+        b.big_next, n_msgs, out, out_off, b.seg_list, b.seg_count, b.whole_list, b.whole_count, mode);
     return hipGetLastError();
   };
+  auto launch_index_big = [&](hipStream_t st) -> hipError_t { return launch_index_big_set(st, set0, 0u); };
   // The forked path's large-message launch runs alone once the lane walk's
   // side finishes, so it takes a full machine of blocks (7 per CU): CM 9.9 ->
   // 8.85 ms against 512 blocks (A/B on one box, twice; 4096: 8.86).
@@ -2145,17 +2173,16 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     const int v = e ? atoi(e) : 1792;
     return v >= 1 ? (u32)v : 1792u;
   }();
-  auto launch_big = [&](hipStream_t st) -> hipError_t {
-    hipError_t e2 = launch_index_big(st);
+  auto launch_big = [&](hipStream_t st, const BigSet& b, u32 mode) -> hipError_t {
+    hipError_t e2 = launch_index_big_set(st, b, mode);
     if (e2 != hipSuccess) return e2;
     // the large-message blocks only (exit after one atomic when the lists
     // are empty)
     const u32 fork_big_blocks = small_blocks < kBigBlocksFork ? small_blocks : kBigBlocksFork;
     ek<<<fork_big_blocks, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
-        reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
-        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), fork_big_blocks, big_threshold, 0u,
-        keep_hist);
+        reinterpret_cast<const u32*>(b.seg_list), b.seg_count, b.whole_list, b.whole_count, b.exec_next,
+        fork_big_blocks, big_threshold, 0u, keep_hist);
     return hipGetLastError();
   };
   auto launch_small = [&](hipStream_t st) -> hipError_t {
@@ -2182,14 +2209,25 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
                                                                   walk_hist, walk_perm);
       if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    // The huge messages (> kHugeIndexBytes compressed) are walked and
+    // executed on a second side stream, so the other large messages'
+    // execution starts when their own (shorter) walks end instead of after
+    // the longest walk: CM 7.6 -> see DESIGN.md section 5.
     std::lock_guard<std::mutex> lk(side->mu);
     if ((e = hipEventRecord(side->fork, stream)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(side->stream, side->fork, 0)) != hipSuccess) return e;
-    if ((e = launch_big(side->stream)) != hipSuccess) return e;
+    const bool split = kSplitHuge && side->stream2;
+    if (split) {
+      if ((e = hipStreamWaitEvent(side->stream2, side->fork, 0)) != hipSuccess) return e;
+      if ((e = launch_big(side->stream2, set1, 1u)) != hipSuccess) return e;
+      if ((e = hipEventRecord(side->join2, side->stream2)) != hipSuccess) return e;
+    }
+    if ((e = launch_big(side->stream, set0, split ? 2u : 0u)) != hipSuccess) return e;
     if ((e = hipEventRecord(side->join, side->stream)) != hipSuccess) return e;
     if ((e = launch_index(true)) != hipSuccess) return e;
     if ((e = launch_small(stream)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(stream, side->join, 0)) != hipSuccess) return e;
+    if (split && (e = hipStreamWaitEvent(stream, side->join2, 0)) != hipSuccess) return e;
   } else {
     // one stream: pass 1, pass 1b, then one exec launch whose first blocks
     // take the large messages (dispatched first) and the rest one message
