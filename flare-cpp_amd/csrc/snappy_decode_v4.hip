@@ -59,6 +59,11 @@ constexpr int kIdxTagsOne = 32, kIdxTagsPlanned = 24;
 #ifndef FSG_BIG_TWO_WINDOWS
 #define FSG_BIG_TWO_WINDOWS 1
 #endif
+// The tag-start bitmap is written whole by the index passes instead of
+// zeroed by the launch (see the lane walk's group stores).
+#ifndef FSG_BITMAP_NOZERO
+#define FSG_BITMAP_NOZERO 1
+#endif
 // Rounds B with pattern chunks outside the common path (see exec5_message).
 #ifndef FSG_ROUNDS_V2
 #define FSG_ROUNDS_V2 1
@@ -593,6 +598,32 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     if (status < 0 && ip == n_in) status = op == expected ? kOk : kCorrupt;
 
     // ---------- store the bit groups the walk has left
+#if FSG_BITMAP_NOZERO
+    // The bitmap is not zeroed by the launch: every group of a message the
+    // execution pass will read is stored here, zero groups included (a
+    // single-literal message's bitmap is never read), and the groups a long
+    // literal jumps over are stored as zeros; at the end the walk's
+    // remaining groups up to the allocation (ceil(n_in / 128)).
+    if (bm && !single_src) {
+      const u32 ngroups = (((n_in + 31) >> 5) + 3) >> 2;
+      const u32 cur = status < 0 ? ip >> 7 : (status == kOk ? ngroups : 0u);
+#pragma unroll
+      for (u32 k = 0; k < kBG; ++k) {
+        const u32 gi = fg + k;
+        if (gi < cur) {
+          const u32 sl = (gi & (kBG - 1)) * 4;
+          u32x4 v;
+#pragma unroll
+          for (u32 q = 0; q < 4; ++q) v[q] = bmr[(sl + q) * kWave + lane];
+          *reinterpret_cast<u32x4*>(bm + 4 * gi) = v;
+#pragma unroll
+          for (u32 q = 0; q < 4; ++q) bmr[(sl + q) * kWave + lane] = 0;
+        }
+      }
+      for (u32 gi = fg + kBG; gi < cur; ++gi) *reinterpret_cast<u32x4*>(bm + 4 * gi) = u32x4{0, 0, 0, 0};
+      fg = cur > fg ? cur : fg;
+    }
+#else
     if (bm) {
       const u32 cur = status < 0 ? ip >> 7 : 0xffffffffu;
 #pragma unroll
@@ -612,6 +643,7 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
       }
       fg = cur > fg + kBG ? cur : (cur > fg ? cur : fg);
     }
+#endif
 
     // ---------- land the chunks loaded last iteration
 #pragma unroll
@@ -672,6 +704,12 @@ __device__ __forceinline__ i32 index_big_message(
   u32 op = 0;
   i32 status = -1;
   u32* bm = bitmap + bm_base[m];
+#if FSG_BITMAP_NOZERO
+  {  // the launch does not zero the bitmap: this message's words first
+    const u32 words = (((n_in + 31) >> 5) + 3) & ~3u;
+    for (u32 wd = 4 * lane; wd < words; wd += 256) *reinterpret_cast<u32x4*>(bm + wd) = u32x4{0, 0, 0, 0};
+  }
+#endif
   const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
   const u8* abase = ib - ibal;
   const u32 last_chunk = (ibal + n_in - 1) >> 4;
@@ -2086,7 +2124,13 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   // lists between them are 20 B per message (A/B: C2 0.159 -> 0.157 ms, C3
   // and CM neutral; a zeroing kernel in place of the runtime fill makes the
   // next index pass place its one-wave workgroups unevenly: C3 +0.27 ms)
+#if FSG_BITMAP_NOZERO
+  // counters and lists only: the passes that write the bitmap store every
+  // word the execution pass reads (C3: an 80 us fill of 267 MB saved)
+  hipError_t e = hipMemsetAsync(w, 0, 256 + kListBases * base_bytes, stream);
+#else
   hipError_t e = hipMemsetAsync(w, 0, 256 + kListBases * base_bytes + cap_words * 4, stream);
+#endif
   if (e != hipSuccess) return e;
   // Large-message threshold: 4x the batch's mean compressed size (estimated
   // from the workspace, which callers size from the packed input), clamped
