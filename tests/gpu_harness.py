@@ -45,9 +45,11 @@ class GpuCodec:
         return [out[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() for i in range(n)], st
 
     def decompress(self, comps: list[bytes], caps: list[int], flags: int = 0,
-                   ws_total_in: int | None = None):
+                   ws_total_in: int | None = None, ws_fill: int | None = None):
         """ws_total_in: input size the workspace is sized for (default: the
-        real packed size; smaller values force the v4 fallback path)."""
+        real packed size; smaller values force the v4 fallback path).
+        ws_fill: byte the workspace is filled with before the call (the
+        decoder must not rely on a zeroed workspace)."""
         torch = self.torch
         b = fsg.Batch.from_list(comps)
         n = len(b)
@@ -58,6 +60,8 @@ class GpuCodec:
         d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
         total_in = int(b.data.size) if ws_total_in is None else ws_total_in
         ws = self.codec.decompress_workspace(n, total_in) if self.use_workspace else None
+        if ws is not None and ws_fill is not None:
+            ws.fill_(ws_fill)
         self.codec.decompress(dev(b.data), dev(b.offsets), dev(b.lens), n, d_out, dev(oo), dev(caps),
                               d_ol, d_st, flags=flags, workspace=ws)
         torch.cuda.synchronize()

@@ -603,3 +603,41 @@ def test_two_stream_decode_stream_of_batches(gpu, oracle):
             assert (st[i] == fsg.FSG_OK) == bool(ok), (k, i, st[i])
             if ok:
                 assert outs[i][:ulen] == ref, (k, i)
+
+
+@pytest.mark.parametrize("fork", ["0", "1"])
+@pytest.mark.parametrize("fill", [0xFF, 0x5A])
+def test_decode_with_garbage_workspace(gpu, oracle, fork, fill, monkeypatch):
+    """The launch zeroes only the workspace's counters and lists: the index
+    passes must store every bitmap word the execution pass reads (zero words,
+    the words a long literal jumps over, the tail up to the allocation;
+    pass 1b its whole message).  Decode with the workspace filled with
+    garbage: text of many sizes, long literals inside text, single-literal
+    and large (pass 1b) bodies, intact and corrupted, against the oracle."""
+    monkeypatch.setenv("FSG_DECODE_FORK", fork)
+    rng = np.random.default_rng(fill)
+    srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0)
+            for s in (1, 33, 200, 1000, 4096, 9000, 65536, 70000, 200000)]
+    srcs += [fsg.make_batch(fsg.KIND_RANDOM, [s], first_index=s).item(0) for s in (100, 5000, 65536, 600000)]
+    # text with random runs inside: long literals between copies
+    for k in range(4):
+        t = bytearray(fsg.make_batch(fsg.KIND_TEXT, [30000], first_index=50 + k).item(0))
+        r = fsg.make_batch(fsg.KIND_RANDOM, [2000 + 3000 * k], first_index=60 + k).item(0)
+        pos = int(rng.integers(0, len(t)))
+        srcs.append(bytes(t[:pos]) + r + bytes(t[pos:]))
+    comps, caps = [], []
+    for i in range(240):
+        c = bytearray(oracle.compress(srcs[i % len(srcs)]))
+        if i % 5 == 4:
+            c[int(rng.integers(len(c)))] ^= 0x41
+        comps.append(bytes(c))
+        caps.append(1 << 19)
+    outs, ol, st = gpu.decompress(comps, caps, ws_fill=fill)
+    for i, (c, o, s) in enumerate(zip(comps, outs, st)):
+        ok, ulen, ref = oracle.uncompress(c, cap=1 << 19)
+        if ok is None:
+            assert s == fsg.FSG_SLOT_TOO_SMALL, i
+        elif not ok:
+            assert s in (fsg.FSG_CORRUPT, fsg.FSG_BAD_HEADER), i
+        else:
+            assert s == fsg.FSG_OK and o[:ulen] == ref, i
