@@ -45,6 +45,24 @@ constexpr int kK = FSG_V3_PROBES;  // probes per batch
 #endif
 constexpr int kPostProbes = FSG_V3_POST_PROBES;  // probes per batch right after a copy
 constexpr u32 kWinChunks = 5;      // 80-byte input window
+// Table entries carry a 16-bit fingerprint of the 4 bytes at the stored
+// position (high half; the position is the low half).  A probe whose
+// fingerprint differs from its candidate's cannot match, so it skips the
+// candidate load: about half of the probes fail, and their candidate lines
+// were a quarter of the fetched bytes.  A fingerprint hit is confirmed by
+// the loaded bytes as before, so the parse is unchanged (FSG_V3_FP=0: the
+// reference's u16 position-only entries).
+#ifndef FSG_V3_FP
+#define FSG_V3_FP 1
+#endif
+constexpr bool kFp = FSG_V3_FP;
+#if FSG_V3_FP
+typedef u32 tent;
+#else
+typedef u16 tent;
+#endif
+__device__ __forceinline__ u32 fp_of(u32 x) { return (x * 0x9E3779B1u) & 0xffff0000u; }
+__device__ __forceinline__ tent tab_entry(u32 pos, u32 x) { return (tent)(kFp ? pos | fp_of(x) : pos); }
 constexpr u32 kWinDw = kWinChunks * 4;
 
 __device__ u32x4 g_enc_dummy[2];
@@ -130,13 +148,13 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, u8* out,
     const u64* __restrict__ out_off, u32* __restrict__ out_len,
-    i32* __restrict__ status, u16* __restrict__ tables, u32 table_entries,
+    i32* __restrict__ status, tent* __restrict__ tables, u32 table_entries,
     u32* __restrict__ ctr, const u32* __restrict__ items, u32* __restrict__ sizes, u32 mode,
     u32 region_cap) {
   __shared__ u32 win[(kWinDw + 1) * kWave];
   const u32 lane = threadIdx.x;
   const u32 slot = blockIdx.x * blockDim.x + lane;
-  u16* table = tables + (u64)slot * table_entries;
+  tent* table = tables + (u64)slot * table_entries;
   auto wrd = [&](u32 d) -> u32 { return win[d * kWave + lane]; };
   const bool fallback = mode & kEncFallback;
   const u32 n_items = (fallback || !items) ? 0u : ctr[1];
@@ -190,11 +208,14 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
       const u8* fb = mb + fpos;
       const u32 ht = table_size_for(n);
       const int shift = 32 - (31 - __clz((int)ht));
-      {
+      // zeroed table (snappy.cc:247-271): every entry is position 0
+      auto fill_table = [&](u32 x0) {
+        const u32 e = kFp ? (u32)tab_entry(0, x0) : 0u;
         u32x4* t4 = reinterpret_cast<u32x4*>(table);
-        const u32x4 z = {0, 0, 0, 0};
-        for (u32 i = 0; i < ht / 8; ++i) t4[i] = z;
-      }
+        const u32x4 z = {e, e, e, e};
+        for (u32 i = 0; i < ht * (u32)sizeof(tent) / 16; ++i) t4[i] = z;
+      };
+      if (!kFp) fill_table(0);
       if (n < kInputMarginBytes) {  // snappy.cc:346-347,446-450
         if (!room(n + 5)) { ovf = true; break; }
         op = emit_literal_global(op, fb, n);
@@ -233,6 +254,7 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
         const u32 c = window_chunks(0, g0);
         window_store(c, g0);
       }
+      if (kFp) fill_table(rd32(0));
 
       u32 ip = 1, next_emit = 0, skip = 32;
       bool post = false;
@@ -292,27 +314,32 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
           X[k] = live[k] ? rd32(P[k]) : 0u;
           H[k] = hash_bytes(X[k], shift);
         }
-        const u32 hpre = post ? hash_bytes(rd32(ip - 1), shift) : 0u;
+        const u32 xpre = post ? rd32(ip - 1) : 0u;
+        const u32 hpre = post ? hash_bytes(xpre, shift) : 0u;
         // ---- round trip 1: table entries
         u32 T[kK];
 #pragma unroll
         for (int k = 0; k < kK; ++k) T[k] = table[live[k] ? H[k] : 0u];
-        // candidates: the sequential read-then-write order, resolved in registers
+        // candidates: the sequential read-then-write order, resolved in
+        // registers; need[k]: the candidate may match, its bytes are loaded
         u32 C[kK];
+        bool need[kK];
 #pragma unroll
         for (int k = 0; k < kK; ++k) {
-          u32 c = T[k];
-          if (post && hpre == H[k]) c = ip - 1;
+          u32 c = T[k] & 0xffffu;
+          bool mb = !kFp || (T[k] & 0xffff0000u) == fp_of(X[k]);
+          if (post && hpre == H[k]) { c = ip - 1; mb = xpre == X[k]; }
 #pragma unroll
           for (int j = 0; j < k; ++j)
-            if (live[j] && H[j] == H[k]) c = P[j];
+            if (live[j] && H[j] == H[k]) { c = P[j]; mb = X[j] == X[k]; }
           C[k] = c;
+          need[k] = live[k] && mb;
         }
         // ---- round trip 2: candidate bytes + next window
         u32x4 CB[kK];
 #pragma unroll
         for (int k = 0; k < kK; ++k) {
-          const u8* a = live[k] ? fb + C[k] : reinterpret_cast<const u8*>(g_enc_dummy);
+          const u8* a = need[k] ? fb + C[k] : reinterpret_cast<const u8*>(g_enc_dummy);
           __builtin_memcpy(&CB[k], a, 16);
         }
         // refresh the window from lo_need only once half of it is consumed:
@@ -326,12 +353,12 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
         int win_k = -1;
 #pragma unroll
         for (int k = kK - 1; k >= 0; --k)
-          if (live[k] && CB[k][0] == X[k]) win_k = k;
+          if (need[k] && CB[k][0] == X[k]) win_k = k;
         // commit table writes (program order)
-        if (post) table[hpre] = (u16)(ip - 1);
+        if (post) table[hpre] = tab_entry(ip - 1, xpre);
 #pragma unroll
         for (int k = 0; k < kK; ++k)
-          if (live[k] && (win_k < 0 || k <= win_k)) table[H[k]] = (u16)P[k];
+          if (live[k] && (win_k < 0 || k <= win_k)) table[H[k]] = tab_entry(P[k], X[k]);
 
         if (win_k >= 0) {
           u32 p = P[0], cand = C[0];
@@ -519,7 +546,7 @@ size_t encode_tables_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out)
   slots = (slots + 255) / 256 * 256;
   if (slots == 0) slots = 256;
   if (slots_out) *slots_out = slots;
-  return 256 + (size_t)slots * entries * sizeof(u16);
+  return 256 + (size_t)slots * entries * sizeof(tent);
 }
 
 size_t encode_plan_bytes(u32 n_msgs, u32 max_in_len) {
@@ -536,7 +563,7 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
                             hipStream_t stream) {
   if (n_msgs == 0) return hipSuccess;
   u32* ctr = reinterpret_cast<u32*>(ws);
-  u16* tables = reinterpret_cast<u16*>(reinterpret_cast<u8*>(ws) + 256);
+  tent* tables = reinterpret_cast<tent*>(reinterpret_cast<u8*>(ws) + 256);
   hipError_t e = hipMemsetAsync(ctr, 0, 256, stream);
   if (e != hipSuccess) return e;
   const size_t plan = encode_plan_bytes(n_msgs, max_in_len);
