@@ -39,11 +39,21 @@ namespace {
 #ifndef FSG_V3_PROBES
 #define FSG_V3_PROBES 3
 #endif
-constexpr int kK = FSG_V3_PROBES;  // probes per batch
+constexpr int kKFlat = FSG_V3_PROBES;  // probes per batch
 #ifndef FSG_V3_POST_PROBES
 #define FSG_V3_POST_PROBES 1
 #endif
-constexpr int kPostProbes = FSG_V3_POST_PROBES;  // probes per batch right after a copy
+constexpr int kPostFlat = FSG_V3_POST_PROBES;  // probes per batch right after a copy
+// Batches with split messages (> 64 KiB) end in a few long fragment chains
+// running alone, bound by each chain's round trips: more probes per batch
+// there (C5 56.1 -> 52.9 ms; on C3, where every lane stays busy, the extra
+// probes' traffic costs 108 -> 118 ms).
+#ifndef FSG_V3_PROBES_SPLIT
+#define FSG_V3_PROBES_SPLIT 4
+#endif
+#ifndef FSG_V3_POST_PROBES_SPLIT
+#define FSG_V3_POST_PROBES_SPLIT 2
+#endif
 constexpr u32 kWinChunks = 5;      // 80-byte input window
 // Table entries carry a 16-bit fingerprint of the 4 bytes at the stored
 // position (high half; the position is the low half).  A probe whose
@@ -144,6 +154,7 @@ __device__ __forceinline__ u8* emit_literal_global(u8* op, const u8* lit, u32 le
 // (FSG_ENC_FALLBACK) re-encodes those messages whole, one lane each.
 constexpr u32 kEncFallback = 1u;
 
+template <int kK, int kPostProbes>
 __global__ __launch_bounds__(64) void encode_pipe_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, u8* out,
@@ -580,17 +591,18 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
                                                                  frag_base, big_list);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  encode_pipe_kernel<<<slots / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off,
-                                                    out_len, status, tables, entries, ctr, items,
-                                                    sizes, 0u, region_cap);
+  auto pipe = max_in_len > kBlockSize || max_in_len == 0
+                  ? encode_pipe_kernel<FSG_V3_PROBES_SPLIT, FSG_V3_POST_PROBES_SPLIT>
+                  : encode_pipe_kernel<kKFlat, kPostFlat>;
+  pipe<<<slots / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off, out_len, status,
+                                      tables, entries, ctr, items, sizes, 0u, region_cap);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (items) {
     encode_gather_kernel<<<1024, 256, 0, stream>>>(in_len, out, out_off, out_len, status, ctr,
                                                    frag_base, big_list, sizes, region_cap);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    encode_pipe_kernel<<<slots / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off,
-                                                      out_len, status, tables, entries, ctr, nullptr,
-                                                      nullptr, kEncFallback, 0u);
+    pipe<<<slots / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off, out_len, status,
+                                        tables, entries, ctr, nullptr, nullptr, kEncFallback, 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;

@@ -502,14 +502,15 @@ def test_mutations_and_trailing_tags(gpu, oracle):
     assert n_ok > 40 and n_bad > 40
 
 
-@pytest.mark.parametrize("keep", ["512", "768", "1024"])
+@pytest.mark.parametrize("keep", ["512", "768", "1024", "2000"])
 def test_window_slide_flush_rule(gpu, oracle, keep, monkeypatch):
     """A window slide must leave every byte a far piece can read in global
     memory: the piece's source lies below the new base but its 16-byte load
     reaches up to 15 bytes above it, so the slide flushes (and waits) when
-    the flush lag leaves fewer than 16 stored bytes at the base.  With the
-    default 2 KiB of kept history that lag is rare; a smaller history
-    (FSG_EXEC_KEEP) makes it frequent.  Before the rule covered the 16
+    the flush lag leaves fewer than 16 stored bytes at the base.  1024 is the
+    shipped default (FSG_KEEP, 3 KiB window) and 2000 the largest history the
+    window allows (kMaxKeep); a smaller history (FSG_EXEC_KEEP) makes the
+    short-lag slide frequent.  Before the rule covered the 16
     bytes, 512 B decoded a zero at offset 343,000 of the 1 MiB golden text.
     Golden vectors (up to 1 MiB, segmented and whole), window-edge streams
     and a C3-like batch, byte-equal to the inputs."""
