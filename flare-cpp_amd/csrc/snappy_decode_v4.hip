@@ -222,6 +222,30 @@ __device__ __forceinline__ u32 pattern_pieces(u32 len, u32 step) {
 
 // ===========================================================================
 // Pass 1: index + validate.  One lane per message.
+// Bump allocation of `total` (this wave's sum) from *counter with one atomic
+// per workgroup: every thread of the block calls it; blk is LDS scratch of
+// (waves + 1) words.  Returns the wave's base.  A device-scope atomic on one
+// address is serialised across the chip: one per wave cost the 1M-message
+// plan pass ~0.25 ms.
+__device__ __forceinline__ u32 block_bump(u32 total, u32* counter, u32* blk) {
+  const u32 wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) blk[wv] = total;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u32 t = 0;
+    for (u32 w = 0; w < nw; ++w) {
+      const u32 x = blk[w];
+      blk[w] = t;
+      t += x;
+    }
+    blk[nw] = t ? atomicAdd(counter, t) : 0u;
+  }
+  __syncthreads();
+  const u32 r = blk[nw] + blk[wv];
+  __syncthreads();
+  return r;
+}
+
 // ===========================================================================
 // Per-lane start of pass 1 (one message per lane, the whole wave calling):
 // header (ReadUncompressedLength / Parse32WithLimit), slot check, the
@@ -233,7 +257,7 @@ __device__ __forceinline__ i32 index_prologue(
     const u32* __restrict__ out_cap, u32* __restrict__ out_len, u32* __restrict__ bm_counter,
     u32* __restrict__ bm_base_out, u32* __restrict__ bitmap, u64 bm_capacity_words,
     u32* __restrict__ big_count, u32* __restrict__ big_list, u32 big_threshold, u32* ip,
-    u32* expected, u32* bm_base_ret) {
+    u32* expected, u32* bm_base_ret, u32* blk = nullptr) {
   const bool strict = flags & 2u;
   const bool validate = flags & 1u;
   i32 status = kOk;  // < 0: parsing
@@ -259,8 +283,12 @@ __device__ __forceinline__ i32 index_prologue(
     const u32 incl = wave_incl_scan(words);
     const u32 total = readlane(incl, 63);
     u32 base0 = 0;
-    if (lane == 0 && total) base0 = atomicAdd(bm_counter, total);
-    base0 = readlane(base0, 0);
+    if (blk) {
+      base0 = block_bump(total, bm_counter, blk);
+    } else {
+      if (lane == 0 && total) base0 = atomicAdd(bm_counter, total);
+      base0 = readlane(base0, 0);
+    }
     bm_base = base0 + incl - words;
     if (status < 0 && (u64)bm_base + words > bm_capacity_words) status = kNeedFallback;
     if (valid_msg) bm_base_out[m] = bm_base;
@@ -304,7 +332,8 @@ __device__ __forceinline__ u32 walk_class(u32 n_in) {
 // the prologue alone, so pass 1b can start on the listed large messages while
 // the lane walk (index_kernel<true>) runs; lanes left for the walk get
 // kNeedLaneWalk.
-__global__ __launch_bounds__(64) void index_plan_kernel(
+constexpr u32 kPlanThreads = 1024;
+__global__ __launch_bounds__(kPlanThreads) void index_plan_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, const u32* __restrict__ out_cap,
     u32* __restrict__ out_len, i32* __restrict__ status_out, u32 flags,
@@ -312,15 +341,19 @@ __global__ __launch_bounds__(64) void index_plan_kernel(
     u32* __restrict__ bitmap, u64 bm_capacity_words, u32* __restrict__ big_count,
     u32* __restrict__ big_list, u32 big_threshold, u32* __restrict__ walk_rank,
     u32* __restrict__ walk_hist) {
+  __shared__ u32 blk[kPlanThreads / 64 + 1];
+  __shared__ u32 hist[kWalkClasses], hbase[kWalkClasses];
   const u32 lane = threadIdx.x & 63;
-  const u32 m = blockIdx.x * 64 + lane;
+  const u32 m = blockIdx.x * kPlanThreads + threadIdx.x;
   const bool valid_msg = m < n_msgs;
   const u8* ib = valid_msg ? in + in_off[m] : in;
   const u32 n_in = valid_msg ? in_len[m] : 0u;
   u32 ip = 0, expected = 0, bm_base = 0;
+  if (threadIdx.x < kWalkClasses) hist[threadIdx.x] = 0;
+  __syncthreads();
   const i32 st = index_prologue(ib, n_in, valid_msg, m, lane, n_msgs, flags, out_cap, out_len,
                                 bm_counter, bm_base_out, bitmap, bm_capacity_words, big_count,
-                                big_list, big_threshold, &ip, &expected, &bm_base);
+                                big_list, big_threshold, &ip, &expected, &bm_base, blk);
   if (valid_msg) status_out[m] = st < 0 ? kNeedLaneWalk : st;
   if (!walk_rank) return;
   // Size classes for the lane walk (a wave's walk lasts as long as its
@@ -336,10 +369,18 @@ __global__ __launch_bounds__(64) void index_plan_kernel(
     if (lane == c) mine = cnt;
     if (cls == c) below_mask_cnt = (u32)__builtin_popcountll(b & ((1ull << lane) - 1));
   }
+  // per-class ranks: this wave's base inside the block (LDS atomics), then
+  // one global atomic per class per block
   u32 base = 0;
-  if (lane < kWalkClasses && mine) base = atomicAdd(&walk_hist[lane], mine);
+  if (lane < kWalkClasses && mine) base = atomicAdd(&hist[lane], mine);
+  __syncthreads();
+  if (threadIdx.x < kWalkClasses) {
+    const u32 h = hist[threadIdx.x];
+    hbase[threadIdx.x] = h ? atomicAdd(&walk_hist[threadIdx.x], h) : 0u;
+  }
+  __syncthreads();
   base = (u32)__shfl((int)base, (int)(cls & (kWalkClasses - 1)), 64);
-  if (walk) walk_rank[m] = base + below_mask_cnt;
+  if (walk) walk_rank[m] = hbase[cls & (kWalkClasses - 1)] + base + below_mask_cnt;
 }
 
 // Class offsets of the size-ordered lane walk (one block): exclusive prefix
@@ -2243,7 +2284,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   if (side) {
     // the plan pass lists the large messages; pass 1b starts on them while
     // the lane walk runs
-    index_plan_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(
+    index_plan_kernel<<<(n_msgs + kPlanThreads - 1) / kPlanThreads, kPlanThreads, 0, stream>>>(
         in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
         cap_words, big_count, big_list, big_threshold, kWalkOrder ? walk_rank : nullptr, walk_hist);
     if ((e = hipGetLastError()) != hipSuccess) return e;
