@@ -81,6 +81,16 @@ constexpr u32 kAhead = 7;                    // chunks prefetched per iteration
 #endif
 constexpr u32 kIdxWaves = FSG_IDX_WAVES;
 static_assert(kIdxWaves == 1 || kIdxWaves == 2 || kIdxWaves == 4, "tag table init");
+// The one-stream lane walk of batches of short bodies (mean compressed size
+// < 16 KiB, e.g. C2) runs four waves per workgroup so its bitmap allocation
+// takes one device-scope atomic per workgroup instead of one per wave: C2
+// 0.1354 -> 0.1276 ms; with long walks (C3) the one-wave blocks stay ahead
+// (6.02 vs 6.06 ms).
+#ifndef FSG_IDX_WAVES_SERIAL
+#define FSG_IDX_WAVES_SERIAL 4
+#endif
+constexpr u32 kIdxWavesSerial = FSG_IDX_WAVES_SERIAL;
+static_assert(kIdxWavesSerial == 1 || kIdxWavesSerial == 2 || kIdxWavesSerial == 4, "tag table init");
 
 // ---- pass 1b (index_big_message, run by exec_kernel's large-message waves) geometry
 constexpr u32 kBigIndexMin = 8 * 1024;       // large: compressed size above
@@ -404,8 +414,8 @@ __global__ __launch_bounds__(256) void walk_scatter_kernel(
 
 // kPlanned: index_plan_kernel ran first (statuses, bitmap bases and the
 // large-message list are in place; only kNeedLaneWalk messages are walked).
-template <bool kPlanned, bool kLean = false>
-__global__ __launch_bounds__(64 * kIdxWaves)
+template <bool kPlanned, bool kLean = false, u32 kW = kIdxWaves>
+__global__ __launch_bounds__(64 * kW)
 __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
     const u32* __restrict__ in_len, u32 n_msgs, const u32* __restrict__ out_cap,
@@ -429,13 +439,13 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   // for the occupancy that LDS alone would allow (97 registers reserved for
   // 52 used), too many to fit beside the execution pass's waves.
   extern __shared__ u32 idx_dyn_lds[];
-  __shared__ u32 ring_s[kLean ? 1 : kIdxWaves][kLean ? 1 : (kRD + 5) * kWave];
+  __shared__ u32 ring_s[kLean ? 1 : kW][kLean ? 1 : (kRD + 5) * kWave];
   __shared__ u32 tagtab_s[kLean ? 1 : 256];
-  __shared__ u32 bmr_s[kLean ? 1 : kIdxWaves][kLean ? 1 : kBW * kWave];
+  __shared__ u32 bmr_s[kLean ? 1 : kW][kLean ? 1 : kBW * kWave];
   const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   u32* const ring = kLean ? idx_dyn_lds + wv * (kRD + 5) * kWave : ring_s[wv];
-  u32* const tagtab = kLean ? idx_dyn_lds + kIdxWaves * (kRD + 5) * kWave : tagtab_s;
-  u32* const bmr = kLean ? idx_dyn_lds + kIdxWaves * (kRD + 5) * kWave + 256 + wv * kBW * kWave : bmr_s[wv];
+  u32* const tagtab = kLean ? idx_dyn_lds + kW * (kRD + 5) * kWave : tagtab_s;
+  u32* const bmr = kLean ? idx_dyn_lds + kW * (kRD + 5) * kWave + 256 + wv * kBW * kWave : bmr_s[wv];
 
   const u32 lane = threadIdx.x & 63;
   // Tag table (the role of char_table, snappy.cc:516-549): per tag byte c,
@@ -444,8 +454,8 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   // literal, 8-15 advance without a long literal's length, 16-23 length
   // (short literal / copies).
 #pragma unroll
-  for (u32 q = 0; q < 4 / kIdxWaves; ++q) {
-    const u32 c = threadIdx.x * (4 / kIdxWaves) + q, type = c & 3, l0 = (c >> 2) + 1;
+  for (u32 q = 0; q < 4 / kW; ++q) {
+    const u32 c = threadIdx.x * (4 / kW) + q, type = c & 3, l0 = (c >> 2) + 1;
     u32 nb, len, lit = 0, ll = 0;
     if (type == 0) {
       lit = 1;
@@ -476,9 +486,10 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   u32 expected = 0, ip = 0, bm_base = 0;
   i32 status = kOk;
   if (!kPlanned) {
+    __shared__ u32 blk_s[kW + 1];
     status = index_prologue(ib, n_in, valid_msg, m, lane, n_msgs, flags, out_cap, out_len,
                             bm_counter, bm_base_out, bitmap, bm_capacity_words, big_count, big_list,
-                            big_threshold, &ip, &expected, &bm_base);
+                            big_threshold, &ip, &expected, &bm_base, kW > 1 ? blk_s : nullptr);
   } else if (valid_msg && status_out[m] == kNeedLaneWalk) {
     u32 ulen = 0;
     ip = (u32)parse_varint_header(ib, n_in, flags & 2u, &ulen);  // valid: checked by the plan
@@ -2189,6 +2200,11 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
           cap_words, big_count, big_list, big_threshold, kWalkOrder ? walk_perm : nullptr, walk_hist);
     else if (two && kLeanWalk)
       index_kernel<false, true><<<idx_blocks, 64 * kIdxWaves, idx_lean_lds_bytes(), stream>>>(
+          in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
+          cap_words, big_count, big_list, big_threshold, nullptr, nullptr);
+    else if (est_total_in < 16384ull * n_msgs)
+      index_kernel<false, false, kIdxWavesSerial><<<(n_msgs + 64 * kIdxWavesSerial - 1) / (64 * kIdxWavesSerial),
+                                                    64 * kIdxWavesSerial, 0, stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
           cap_words, big_count, big_list, big_threshold, nullptr, nullptr);
     else
