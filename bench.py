@@ -268,13 +268,19 @@ def rank_main(args, codec_factory=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gpu = args.device == "cuda"
+    # Test knob (tests/test_gpu_multirank.py): every rank on this one device
+    # with gloo collectives, so the N-rank path runs the HIP codec on a
+    # one-GPU box (RCCL refuses two ranks on one device).  Never a bench line.
+    shared = os.environ.get("FSG_BENCH_SHARED_DEVICE")
     if gpu:
+        local = int(shared) if shared is not None else local
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
+    backend = "nccl" if gpu and shared is None else "gloo"
     if world > 1:
-        dist.init_process_group("nccl" if gpu else "gloo", init_method="env://")
+        dist.init_process_group(backend, init_method="env://")
         world = dist.get_world_size()
     codec = codec_factory(local) if codec_factory else fsg.SnappyGPU(local)
     if args.decode_kernel or args.encode_kernel:  # else the library's choice (FSG_DECODE_KERNEL env)
@@ -485,7 +491,8 @@ def rank_main(args, codec_factory=None):
                 "parallelism": f"shard{world} ({scaling}: messages by index"
                                f"{', byte-balanced' if scaling == 'strong' else ''}; no data-path collective)",
                 "world_size_seen_by_collectives": world,
-                "backend": ("nccl (RCCL over xGMI)" if gpu else "gloo") if world > 1 else None,
+                "backend": ("nccl (RCCL over xGMI)" if backend == "nccl" else
+                            "gloo" + (" (shared device, test)" if shared is not None else "")) if world > 1 else None,
             },
             "roofline": {
                 "bound": "hbm",
