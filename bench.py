@@ -333,8 +333,10 @@ def rank_main(args, codec_factory=None):
             for i in idx)
         del host_comp
 
-    # Decode output slots (exact uncompressed sizes) -- laid out like the raw batch.
-    d_out = torch.zeros(max(raw_total, 1), dtype=torch.uint8, device=dev)
+    # Decode output slots (exact uncompressed sizes) -- laid out like the raw
+    # batch, poisoned (0xA5) so a byte the decoder never writes fails the
+    # round-trip check even where its true value is 0.
+    d_out = torch.full((max(raw_total, 1),), 0xA5, dtype=torch.uint8, device=dev)
     d_out_len = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
     d_dws = codec.decompress_workspace(n, c_tot)
 
@@ -377,7 +379,7 @@ def rank_main(args, codec_factory=None):
             sample_ok = sample_ok and all(
                 host_comp2[int(c2_off[i]):int(c2_off[i]) + int(comp_len2[i])].tobytes()
                 == orc.compress(batch2.item(int(i))) for i in idx)
-        d_out2 = torch.zeros(max(batch2.total, 1), dtype=torch.uint8, device=dev)
+        d_out2 = torch.full((max(batch2.total, 1),), 0xA5, dtype=torch.uint8, device=dev)
         d_out_len2 = torch.zeros(n, dtype=torch.int32, device=dev)
         d_dws2 = codec.decompress_workspace(n, c2_tot)
         slots = [

@@ -1165,8 +1165,20 @@ __device__ __forceinline__ void init_mask_table(u32x4* mtab, u32 t) {
 // ("far copies").  src + 16 <= op <= the slot length
 // (far sources end >= 16 bytes below the window base, which is <= op - 16), so
 // the range check never clips a needed byte.
+#ifdef FSG_DIAG_FAR_FIXED
+// Diagnostic build only (wrong output, timing only): every far load reads one
+// fixed, L2-resident 64-byte line instead of the slot, so the far copies
+// cost their instructions but no memory traffic.
+__device__ u32x4 g_far_line[4];
+#endif
 __device__ __forceinline__ u32x4 far_load(__amdgpu_buffer_rsrc_t r, u32 off) {
+#ifdef FSG_DIAG_FAR_FIXED
+  (void)r;
+  const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc(g_far_line, (short)0, 64, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b128(fr, off & 48u, 0, 0);
+#else
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+#endif
 }
 
 // One message, executed by the calling wave (see the pass-2 comment above).
@@ -1949,8 +1961,11 @@ __device__ __forceinline__ void exec5_message(
 #endif
 }
 
-// 6 waves per SIMD (62 VGPRs, LDS 25 KB per block); 7 waves (smaller tag ring
-// or window) and larger windows at 3-4 waves were slower.
+// 7 waves per SIMD by default (FSG_EXEC_WAVES; 72 VGPRs, 22.2 KB of LDS per
+// block with the 3 KiB window: C3 6.35 -> 6.20 ms against 6 waves with a
+// 4 KiB window, A/B on one box; 8 waves spill and were slower).
+// The v4 variant (exec_kernel<4>) shares the setting and was not re-measured
+// at 7.
 // The first kBigBlocks blocks take the large messages listed by pass 1 from a
 // device counter (blocks dispatch in order, so the longest messages start
 // first); every other block runs the wave-per-message mapping and skips them.
@@ -2064,10 +2079,41 @@ __global__ __launch_bounds__(64) void fallback_kernel(
   status[m] = decode_one(ib + h, ib + n_in, out + out_off[m], out_len[m], true);
 }
 
-// Workspace: [0, 256) counters (bitmap bump allocator at 0, large-message
-// count at 64, huge-message count at 96, queue heads at 128 and 192, segment
-// count at 160, whole-message count at 224) | bm_base[n] | big_list[n] |
-// seg_list[n] (u64) | whole_list[n] | bitmap words.
+// Workspace layout (bytes from the start; every counter a u32, zeroed by the
+// launch's one fill together with the lists):
+//   [0, 256)  counters, at the kWs* offsets below
+//   then kListBases arrays of base_bytes = round_up(4 n, 256) bytes each:
+//     0 bm_base[n] | 1 big_list[n] | 2-3 seg_list[n] (u64) | 4 whole_list[n] |
+//     5 walk_rank[n] | 6 walk_perm[n] | 7 walk_hist (16 classes + count) |
+//     8-9 seg_list2[n] (u64) | 10 whole_list2[n]
+//   then the tag-start bitmap words.
+// Set 0 = every large message (one stream) or the non-huge ones (forked);
+// set 1 = the huge ones (forked, second side stream).
+constexpr u32 kWsBmCounter = 0;        // bitmap bump allocator
+constexpr u32 kWsSet1BigNext = 16;     // set 1: pass-1b work counter
+constexpr u32 kWsSet1SegCount = 32;    // set 1: segment count
+constexpr u32 kWsSet1WholeCount = 48;  // set 1: whole-message count
+constexpr u32 kWsBigCount = 64;        // large-message count (huge count at +32: big_count + 8)
+constexpr u32 kWsHugeCount = kWsBigCount + 32;
+constexpr u32 kWsSet0BigNext = 128;
+constexpr u32 kWsSet0SegCount = 160;
+constexpr u32 kWsSet0ExecNext = 192;   // pass-2 queue head
+constexpr u32 kWsSet0WholeCount = 224;
+constexpr u32 kWsSet1ExecNext = 240;
+constexpr u32 kWsCounterBytes = 256;
+// the counters are distinct u32 slots inside the 256-byte header
+constexpr u32 kWsOffsets[] = {kWsBmCounter, kWsSet1BigNext, kWsSet1SegCount, kWsSet1WholeCount, kWsBigCount,
+                              kWsHugeCount, kWsSet0BigNext, kWsSet0SegCount, kWsSet0ExecNext, kWsSet0WholeCount,
+                              kWsSet1ExecNext};
+constexpr bool ws_offsets_ok() {
+  for (u32 i = 0; i < sizeof(kWsOffsets) / sizeof(kWsOffsets[0]); ++i) {
+    if (kWsOffsets[i] % 4 || kWsOffsets[i] + 4 > kWsCounterBytes) return false;
+    for (u32 j = 0; j < i; ++j)
+      if (kWsOffsets[i] < kWsOffsets[j] + 4 && kWsOffsets[j] < kWsOffsets[i] + 4) return false;
+  }
+  return true;
+}
+static_assert(ws_offsets_ok(), "workspace counters overlap or leave the header");
 constexpr u64 kListBases = 11;  // u32 arrays of n entries before the bitmap
 size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
@@ -2124,7 +2170,18 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   SideStream* two = nullptr;
   if (pass1_stream && pass1_stream != stream) {
     two = side_stream();
-    if (!two) return hipErrorNotReady;
+    if (!two) {
+      // No per-device event set: order `stream` behind whatever the caller
+      // queued on pass1_stream with a temporary event and run every pass on
+      // `stream` (as capi.hip's single-pass path does).
+      hipEvent_t ev = nullptr;
+      hipError_t e0 = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      if (e0 == hipSuccess) e0 = hipEventRecord(ev, pass1_stream);
+      if (e0 == hipSuccess) e0 = hipStreamWaitEvent(stream, ev, 0);
+      if (ev) (void)hipEventDestroy(ev);
+      if (e0 != hipSuccess) return e0;
+      pass1_stream = nullptr;
+    }
   }
   hipStream_t const caller_stream = stream;
   // planned lane walk in size-class order (FSG_WALK_ORDER=0 disables)
@@ -2154,8 +2211,8 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   u8* w = static_cast<u8*>(ws);
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
   if (ws_bytes < 256 + kListBases * base_bytes + 4 * 64) return hipErrorInvalidValue;
-  u32* counter = reinterpret_cast<u32*>(w);
-  u32* big_count = reinterpret_cast<u32*>(w + 64);
+  u32* counter = reinterpret_cast<u32*>(w + kWsBmCounter);
+  u32* big_count = reinterpret_cast<u32*>(w + kWsBigCount);
   u32* bm_base = reinterpret_cast<u32*>(w + 256);
   u32* big_list = reinterpret_cast<u32*>(w + 256 + base_bytes);
   u64* seg_list = reinterpret_cast<u64*>(w + 256 + 2 * base_bytes);
@@ -2253,10 +2310,12 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     u64* seg_list;
     u32* whole_list;
   };
-  const BigSet set0{reinterpret_cast<u32*>(w + 128), reinterpret_cast<u32*>(w + 160),
-                    reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), seg_list, whole_list};
-  const BigSet set1{reinterpret_cast<u32*>(w + 16), reinterpret_cast<u32*>(w + 32),
-                    reinterpret_cast<u32*>(w + 48), reinterpret_cast<u32*>(w + 240), seg_list2, whole_list2};
+  const BigSet set0{reinterpret_cast<u32*>(w + kWsSet0BigNext), reinterpret_cast<u32*>(w + kWsSet0SegCount),
+                    reinterpret_cast<u32*>(w + kWsSet0WholeCount), reinterpret_cast<u32*>(w + kWsSet0ExecNext),
+                    seg_list, whole_list};
+  const BigSet set1{reinterpret_cast<u32*>(w + kWsSet1BigNext), reinterpret_cast<u32*>(w + kWsSet1SegCount),
+                    reinterpret_cast<u32*>(w + kWsSet1WholeCount), reinterpret_cast<u32*>(w + kWsSet1ExecNext),
+                    seg_list2, whole_list2};
   auto launch_index_big_set = [&](hipStream_t st, const BigSet& b, u32 mode) -> hipError_t {
     const u32 q = (n_msgs + 3) / 4;
     const u32 blocks = q < 1024u ? q : 1024u;
@@ -2269,8 +2328,8 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   // The forked path's large-message launch runs alone once the lane walk's
   // side finishes, so it takes a full machine of blocks (7 per CU): CM 9.9 ->
   // 8.85 ms against 512 blocks (A/B on one box, twice; 4096: 8.86).
-  static const u32 kBigBlocksFork = [] {
-    const char* e = getenv("FSG_EXEC_BIG_BLOCKS");
+  static const u32 kBigBlocksFork = [] {  // A/B knob, separate from the one-stream launch's
+    const char* e = getenv("FSG_EXEC_BIG_BLOCKS_FORK");
     const int v = e ? atoi(e) : 1792;
     return v >= 1 ? (u32)v : 1792u;
   }();
@@ -2291,9 +2350,8 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     // takes the large-message role)
     ek<<<small_blocks, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
-        reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
-        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), 0u, big_threshold, 0u,
-        keep_hist);
+        reinterpret_cast<const u32*>(seg_list), set0.seg_count, whole_list, set0.whole_count, set0.exec_next,
+        0u, big_threshold, 0u, keep_hist);
     return hipGetLastError();
   };
   SideStream* side = fork ? side_stream() : nullptr;
@@ -2343,9 +2401,8 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     }
     ek<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
-        reinterpret_cast<const u32*>(seg_list), reinterpret_cast<u32*>(w + 160), whole_list,
-        reinterpret_cast<u32*>(w + 224), reinterpret_cast<u32*>(w + 192), big_blocks,
-        big_threshold, kPrio, keep_hist);
+        reinterpret_cast<const u32*>(seg_list), set0.seg_count, whole_list, set0.whole_count, set0.exec_next,
+        big_blocks, big_threshold, kPrio, keep_hist);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // Diagnostic only (FSG_DIAG_NO_TAIL=1): skip this pass to trace the

@@ -547,7 +547,8 @@ __global__ __launch_bounds__(256) void encode_gather_kernel(
 // Plan region after the tables: items (2 x u32 per fragment), per-item
 // sizes, per-message first item, split-message list.
 // Per-lane hash tables for the lane-per-message encoder: [counter: 256 B]
-// [tables: slots x entries x u16], entries per WorkingMemory::GetHashTable
+// [tables: slots x entries x sizeof(tent)] (tent = u32 with FSG_V3_FP, the
+// default: position + fingerprint, twice the u16 footprint), entries per WorkingMemory::GetHashTable
 // (snappy.cc:247-271) for the largest fragment of the batch.
 size_t encode_tables_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out) {
   u32 cap = max_in_len == 0 || max_in_len > kBlockSize ? kBlockSize : max_in_len;

@@ -130,8 +130,10 @@ int fsg_uncompressed_lengths_batch(const uint8_t *d_in, const uint64_t *d_in_off
                                    uint32_t *d_ulen, int lenient, void *stream);
 
 /* Device workspace for fsg_compress_batch: per-lane hash tables (one
- * htsize x u16 table per concurrently encoding lane, htsize per
- * WorkingMemory::GetHashTable, snappy.cc:247-271) plus a work counter.
+ * htsize-entry table per concurrently encoding lane, htsize per
+ * WorkingMemory::GetHashTable, snappy.cc:247-271; 4-byte entries, a position
+ * and its fingerprint, so twice the reference's u16 table: up to 16 GiB at
+ * the 262,144-lane cap with 64 KiB fragments) plus a work counter.
  * max_in_len bounds every message length of the batch (0 = any).  Passing a
  * smaller or NULL workspace selects the LDS-table wave-per-message encoder. */
 size_t fsg_compress_workspace_bytes(uint32_t n_msgs, uint32_t max_in_len);
@@ -180,7 +182,13 @@ int fsg_decompress_batch(const uint8_t *d_in, const uint64_t *d_in_off,
  * issue-bound).  The inputs must be ready on `pass1_stream`; calls that share
  * any of those buffers must be ordered by the caller (pass 1 writes the
  * workspace, d_out_len, d_status and, for messages cut into 64 KiB segments,
- * 4 bytes of d_out).  Results are valid once `stream` is synchronised. */
+ * 4 bytes of d_out).  Results are valid once `stream` is synchronised.
+ * Meant for uniform batches: this form never forks the large-message passes
+ * onto the side streams (fsg_decompress_batch does for batches of more than
+ * 128K messages), so a mixed batch with very large bodies (CM-like) runs its
+ * large-message walk before the execution pass and is faster through
+ * fsg_decompress_batch.  When the library cannot create its per-device
+ * events, `stream` waits on `pass1_stream` and every pass runs on `stream`. */
 int fsg_decompress_batch_2s(const uint8_t *d_in, const uint64_t *d_in_off,
                             const uint32_t *d_in_len, uint32_t n_msgs,
                             uint8_t *d_out, const uint64_t *d_out_off,

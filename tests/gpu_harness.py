@@ -1,10 +1,16 @@
 """Shared GPU-test plumbing: move host batches to the device, run the C ABI,
-bring results back.  torch is used only for device allocations/streams."""
+bring results back.  torch is used only for device allocations/streams.
+
+Output slots are filled with POISON (0xA5) before every call, never zeros: an
+output byte a kernel fails to write then shows up as 0xA5 instead of passing
+whenever its true value happens to be 0."""
 from __future__ import annotations
 
 import numpy as np
 
 import fsg
+
+POISON = 0xA5
 
 
 def dev(a: np.ndarray, device="cuda"):
@@ -31,7 +37,7 @@ class GpuCodec:
         oo, tot = fsg.slot_offsets(caps)
         d_in = dev(batch.data)
         d_io, d_il = dev(batch.offsets), dev(batch.lens)
-        d_out = torch.zeros(tot, dtype=torch.uint8, device="cuda")
+        d_out = torch.full((max(tot, 1),), POISON, dtype=torch.uint8, device="cuda")
         d_oo = dev(oo)
         d_ol = empty(n, torch.int32)
         d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
@@ -55,7 +61,7 @@ class GpuCodec:
         n = len(b)
         caps = np.array(caps, dtype=np.uint32)
         oo, tot = fsg.slot_offsets(caps.astype(np.uint64))
-        d_out = torch.zeros(tot, dtype=torch.uint8, device="cuda")
+        d_out = torch.full((max(tot, 1),), POISON, dtype=torch.uint8, device="cuda")
         d_ol = empty(n, torch.int32)
         d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
         total_in = int(b.data.size) if ws_total_in is None else ws_total_in
@@ -77,7 +83,7 @@ class GpuCodec:
         n = len(batch)
         caps = np.array([self.codec.lib.fsg_lz4_max_compressed_length(int(x)) for x in batch.lens], dtype=np.uint64)
         oo, tot = fsg.slot_offsets(caps)
-        d_out = torch.zeros(tot, dtype=torch.uint8, device="cuda")
+        d_out = torch.full((max(tot, 1),), POISON, dtype=torch.uint8, device="cuda")
         d_ol = empty(n, torch.int32)
         d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
         ws = self.codec.lz4_compress_workspace(n)
@@ -95,7 +101,7 @@ class GpuCodec:
         n = len(b)
         caps = np.array(caps, dtype=np.uint32)
         oo, tot = fsg.slot_offsets(caps.astype(np.uint64))
-        d_out = torch.zeros(tot, dtype=torch.uint8, device="cuda")
+        d_out = torch.full((max(tot, 1),), POISON, dtype=torch.uint8, device="cuda")
         d_ol = empty(n, torch.int32)
         d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
         self.codec.lz4_decompress(dev(b.data), dev(b.offsets), dev(b.lens), n, d_out, dev(oo), dev(caps), d_ol, d_st)

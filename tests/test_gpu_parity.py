@@ -567,7 +567,7 @@ def test_two_stream_decode_stream_of_batches(gpu, oracle):
     slot_bufs = []
     for _ in range(2):
         n = max(s["n"] for s in sets)
-        slot_bufs.append(dict(out=torch.zeros(n << 18, dtype=torch.uint8, device="cuda"),
+        slot_bufs.append(dict(out=torch.full((n << 18,), 0xA5, dtype=torch.uint8, device="cuda"),
                               ol=torch.zeros(n, dtype=torch.int32, device="cuda"),
                               st=torch.full((n,), -7, dtype=torch.int32, device="cuda"),
                               ws=codec.decompress_workspace(n, max(int(s["d_in"].numel()) for s in sets)),
