@@ -33,7 +33,7 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                             u32* out_len, i32* status, void* ws, size_t ws_bytes,
                             u32 slots, u32 entries, size_t tables_bytes, u32 region_cap,
-                            hipStream_t stream);
+                            hipStream_t stream, u32 wave_min);
 hipError_t launch_encode(const u8* in, const u64* in_off, const u32* in_len,
                          u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                          u32* out_len, i32* status, hipStream_t stream);
@@ -58,6 +58,16 @@ int env_int(const char* name) {
 // FSG_ENCODE_KERNEL, changeable with fsg_select_kernels for A/B runs.
 std::atomic<int> g_decode_variant{env_int("FSG_DECODE_KERNEL")};
 std::atomic<int> g_encode_variant{env_int("FSG_ENCODE_KERNEL")};
+// Messages of at least this many bytes (and every fragment of a message over
+// 64 KiB) form the long list, whose units the wave encoder (hash table in
+// LDS, one wave per fragment) and the lane encoder share (wave_quota); the
+// shorter messages go to the lane encoder.  FSG_ENCODE_WAVE_MIN overrides
+// per call (0 = lane encoder only).  Measured on MI355X (A/B, one box): C3
+// compress 108.0 -> 98.4 ms, C5 54.9 -> 39.1 ms.
+fsg::u32 encode_wave_min() {
+  const char* e = getenv("FSG_ENCODE_WAVE_MIN");
+  return e ? (fsg::u32)atoi(e) : 16384u;
+}
 // Test knob: cap the staging region of a split message's fragments (bytes;
 // 0 = slot / fragments).  Small caps force the whole-message fallback pass.
 std::atomic<unsigned> g_region_cap{(unsigned)env_int("FSG_TEST_REGION_CAP")};
@@ -174,7 +184,7 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
                                         d_out_off, d_out_len, d_status, d_workspace,
                                         workspace_bytes, slots, fsg::table_size_for(cap), need,
                                         g_region_cap.load(std::memory_order_relaxed),
-                                        (hipStream_t)stream),
+                                        (hipStream_t)stream, encode_wave_min()),
                   "fsg_compress_batch");
   }
   return record(fsg::launch_encode(d_in, d_in_off, d_in_len, n_msgs, max_in_len,

@@ -83,4 +83,24 @@ __device__ __forceinline__ u32 hash_bytes(u32 bytes, int shift) {
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// ---- encode work units (encode_plan_kernel's long list)
+constexpr u32 kWholeUnit = 0x80000000u;  // unit = a whole message (not a fragment of a split one)
+
+// Units [0, quota) of the long list go to the wave encoder, the rest to the
+// lane encoder.  All of them when their bytes fit what the wave encoder does
+// in about the time one lane needs for a 64 KiB fragment at full load (the
+// lane path's floor: a lane taking a long unit late sets the batch's tail;
+// measured on MI355X: wave encoder ~15.9 GB/s on text, one lane ~40 ms per
+// 64 KiB fragment); otherwise the wave encoder's share of a bandwidth-bound
+// batch (~0.28: 15.9 GB/s beside the lanes' ~40 GB/s).  Both kernels compute
+// it from the plan pass's counters.
+__device__ __forceinline__ u32 wave_quota(const u32* ctr, u32 share_permille, u64 all_bytes) {
+  const u32 n_long = ctr[1];
+  const u64 bytes = *reinterpret_cast<const unsigned long long*>(ctr + 6);
+  if (bytes <= all_bytes) return n_long;
+  const u64 q = ((u64)n_long * share_permille + 999) / 1000;
+  return q < n_long ? (u32)q : n_long;
+}
+
+
 }  // namespace fsg

@@ -32,6 +32,9 @@
 // EmitLiteral / EmitCopy follow snappy.cc:156-232.
 #include "snappy_device.h"
 
+#include <cstdlib>
+#include <mutex>
+
 namespace fsg {
 
 namespace {
@@ -161,27 +164,37 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
     const u64* __restrict__ out_off, u32* __restrict__ out_len,
     i32* __restrict__ status, tent* __restrict__ tables, u32 table_entries,
     u32* __restrict__ ctr, const u32* __restrict__ items, u32* __restrict__ sizes, u32 mode,
-    u32 region_cap) {
+    u32 region_cap, u32 wave_min, u32 wave_share, u64 wave_all_bytes) {
   __shared__ u32 win[(kWinDw + 1) * kWave];
   const u32 lane = threadIdx.x;
   const u32 slot = blockIdx.x * blockDim.x + lane;
   tent* table = tables + (u64)slot * table_entries;
   auto wrd = [&](u32 d) -> u32 { return win[d * kWave + lane]; };
   const bool fallback = mode & kEncFallback;
+  // wave_min != 0: the long list holds the split messages' fragments and the
+  // messages of [wave_min, 64 KiB] bytes; encode_wave_kernel takes its first
+  // `quota` units, the lanes the rest
   const u32 n_items = (fallback || !items) ? 0u : ctr[1];
+  const u32 quota = (fallback || !items || !wave_min) ? 0u : wave_quota(ctr, wave_share, wave_all_bytes);
+  const u32 lane_units = n_items - quota;
 
   for (;;) {
     const u32 w = atomicAdd(&ctr[fallback ? 4 : 0], 1u);
     u32 m, f_first, f_end;     // message, fragment range [f_first, f_end) in bytes
     bool staged = false;       // a fragment of a split message
-    if (w < n_items) {
-      m = items[2 * w];
-      f_first = items[2 * w + 1] << kBlockLog;
-      staged = true;
+    const u32 unit = quota + w;
+    if (w < lane_units) {
+      m = items[2 * unit];
+      const u32 f = items[2 * unit + 1];
+      staged = f != kWholeUnit;
+      f_first = staged ? f << kBlockLog : 0u;
     } else {
-      m = w - n_items;
+      m = w - lane_units;
       if (m >= n_msgs) break;
-      if (fallback ? status[m] != kNeedFallback : (items && in_len[m] > kBlockSize)) continue;
+      if (fallback ? status[m] != kNeedFallback
+                   : ((items && in_len[m] > kBlockSize) ||
+                      (wave_min && in_len[m] >= wave_min && in_len[m] <= kBlockSize)))
+        continue;
       f_first = 0;
     }
     const u8* mb = in + in_off[m];
@@ -454,7 +467,7 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
       }
     }
     if (staged) {
-      sizes[w] = ovf ? 0xffffffffu : (u32)(op - region);
+      sizes[unit] = ovf ? 0xffffffffu : (u32)(op - region);
     } else {
       out_len[m] = (u32)(op - dst);
       status[m] = kOk;
@@ -464,21 +477,33 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
 
 // Lists the fragments of every message longer than one fragment (one item
 // each) and the messages themselves; ctr[1] = items, ctr[2] = split messages.
+// With long_min != 0 (the wave encoder is on) the messages of [long_min,
+// 64 KiB] bytes are listed too, one whole-message unit each (fragment field
+// kWholeUnit), and the bytes of all listed units are summed (ctr[6..7]) for
+// the wave / lane split (wave_quota).
 __global__ void encode_plan_kernel(const u32* __restrict__ in_len, u32 n_msgs,
                                    u32* __restrict__ ctr, u32* __restrict__ items,
-                                   u32* __restrict__ frag_base, u32* __restrict__ big_list) {
+                                   u32* __restrict__ frag_base, u32* __restrict__ big_list, u32 long_min) {
   const u32 m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= n_msgs) return;
   const u32 len = in_len[m];
-  if (len <= kBlockSize) return;
-  const u32 nfr = (len + kBlockSize - 1) >> kBlockLog;
-  const u32 base = atomicAdd(&ctr[1], nfr);
-  frag_base[m] = base;
-  big_list[atomicAdd(&ctr[2], 1u)] = m;
-  for (u32 k = 0; k < nfr; ++k) {
-    items[2 * (base + k)] = m;
-    items[2 * (base + k) + 1] = k;
+  if (len > kBlockSize) {
+    const u32 nfr = (len + kBlockSize - 1) >> kBlockLog;
+    const u32 base = atomicAdd(&ctr[1], nfr);
+    frag_base[m] = base;
+    big_list[atomicAdd(&ctr[2], 1u)] = m;
+    for (u32 k = 0; k < nfr; ++k) {
+      items[2 * (base + k)] = m;
+      items[2 * (base + k) + 1] = k;
+    }
+  } else if (long_min && len >= long_min) {
+    const u32 u = atomicAdd(&ctr[1], 1u);
+    items[2 * u] = m;
+    items[2 * u + 1] = kWholeUnit;
+  } else {
+    return;
   }
+  if (long_min) atomicAdd(reinterpret_cast<unsigned long long*>(ctr + 6), (unsigned long long)len);
 }
 
 // One wave per split message (grid-stride over the list): moves fragments 1..
@@ -544,8 +569,6 @@ __global__ __launch_bounds__(256) void encode_gather_kernel(
   }
 }
 
-// Plan region after the tables: items (2 x u32 per fragment), per-item
-// sizes, per-message first item, split-message list.
 // Per-lane hash tables for the lane-per-message encoder: [counter: 256 B]
 // [tables: slots x entries x sizeof(tent)] (tent = u32 with FSG_V3_FP, the
 // default: position + fingerprint, twice the u16 footprint), entries per WorkingMemory::GetHashTable
@@ -561,18 +584,60 @@ size_t encode_tables_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out)
   return 256 + (size_t)slots * entries * sizeof(tent);
 }
 
+// Plan region: units (2 x u32 each: message, fragment or kWholeUnit), per-unit
+// sizes, per-message first unit, split-message list.  Present when a message
+// may be split (max_in_len > 64 KiB) or may be long enough for the wave
+// encoder (>= kWaveMinBound).  (max_in_len 0 = unknown: no plan, every
+// message encoded whole by one lane.)
+constexpr u32 kWaveMinBound = 4096;  // smallest wave_min the plan region is sized for
 size_t encode_plan_bytes(u32 n_msgs, u32 max_in_len) {
-  if (max_in_len <= kBlockSize) return 0;  // (0 = unknown bound: messages are not split)
-  const u64 per_msg = (max_in_len + kBlockSize - 1) >> kBlockLog;
+  if (max_in_len < kWaveMinBound) return 0;
+  u64 per_msg = ((u64)max_in_len + kBlockSize - 1) >> kBlockLog;
+  if (per_msg < 1) per_msg = 1;
   const u64 max_items = (u64)n_msgs * per_msg;
   return (size_t)(max_items * 12 + (u64)n_msgs * 8 + 256);
 }
+
+__global__ void encode_wave_kernel(const u8* __restrict__ in, const u64* __restrict__ in_off,
+                                   const u32* __restrict__ in_len, u32 n_msgs, u8* out,
+                                   const u64* __restrict__ out_off, u32* __restrict__ out_len,
+                                   i32* __restrict__ status, u32* __restrict__ ctr, const u32* __restrict__ items,
+                                   u32* __restrict__ sizes, u32 region_cap, u32 share_permille, u64 all_bytes);
+
+// Per-device side stream for the wave encoder (created on first use; nullptr:
+// the wave encoder runs on the caller's stream before the lanes).
+namespace {
+struct EncSide {
+  hipStream_t stream = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  std::mutex mu;
+};
+EncSide* enc_side() {
+  constexpr int kMaxDevices = 64;
+  static EncSide g[kMaxDevices];
+  static std::once_flag once[kMaxDevices];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+  EncSide* s = &g[dev];
+  std::call_once(once[dev], [s] {
+    if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&s->fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->join, hipEventDisableTiming) != hipSuccess)
+      s->stream = nullptr;
+  });
+  return s->stream ? s : nullptr;
+}
+u32 env_u32(const char* name, u32 dflt) {
+  const char* e = getenv(name);
+  return e ? (u32)strtoul(e, nullptr, 10) : dflt;
+}
+}  // namespace
 
 hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                             u32* out_len, i32* status, void* ws, size_t ws_bytes,
                             u32 slots, u32 entries, size_t tables_bytes, u32 region_cap,
-                            hipStream_t stream) {
+                            hipStream_t stream, u32 wave_min) {
   if (n_msgs == 0) return hipSuccess;
   u32* ctr = reinterpret_cast<u32*>(ws);
   tent* tables = reinterpret_cast<tent*>(reinterpret_cast<u8*>(ws) + 256);
@@ -580,30 +645,61 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
   if (e != hipSuccess) return e;
   const size_t plan = encode_plan_bytes(n_msgs, max_in_len);
   u32 *items = nullptr, *sizes = nullptr, *frag_base = nullptr, *big_list = nullptr;
-  if (plan && ws_bytes >= tables_bytes + plan) {
-    const u64 per_msg = (max_in_len + kBlockSize - 1) >> kBlockLog;
-    const u64 max_items = (u64)n_msgs * per_msg;
+  const bool can_split = max_in_len > kBlockSize;
+  if (wave_min && wave_min < kWaveMinBound) wave_min = kWaveMinBound;
+  if (max_in_len < wave_min) wave_min = 0;  // nothing long enough (or no bound known)
+  if (plan && ws_bytes >= tables_bytes + plan && (can_split || wave_min)) {
+    const u64 max_items = (plan - 256 - (u64)n_msgs * 8) / 12;
     u8* p = reinterpret_cast<u8*>(ws) + tables_bytes;
     items = reinterpret_cast<u32*>(p);
     sizes = items + 2 * max_items;
     frag_base = sizes + max_items;
     big_list = frag_base + n_msgs;
-    encode_plan_kernel<<<(n_msgs + 255) / 256, 256, 0, stream>>>(in_len, n_msgs, ctr, items,
-                                                                 frag_base, big_list);
+    encode_plan_kernel<<<(n_msgs + 255) / 256, 256, 0, stream>>>(in_len, n_msgs, ctr, items, frag_base, big_list,
+                                                                 wave_min);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+  } else {
+    wave_min = 0;
   }
+  // (read per call: the tests force the lane share with FSG_ENCODE_WAVE_ALL_MB=0)
+  const u32 kShare = env_u32("FSG_ENCODE_WAVE_SHARE", 280);  // permille
+  const u64 kAllBytes = (u64)env_u32("FSG_ENCODE_WAVE_ALL_MB", 640) << 20;
   auto pipe = max_in_len > kBlockSize || max_in_len == 0
                   ? encode_pipe_kernel<FSG_V3_PROBES_SPLIT, FSG_V3_POST_PROBES_SPLIT>
                   : encode_pipe_kernel<kKFlat, kPostFlat>;
-  pipe<<<slots / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off, out_len, status,
-                                      tables, entries, ctr, items, sizes, 0u, region_cap);
+  // The wave encoder's share of the long units (hash table in LDS, one wave
+  // per fragment: snappy_encode_wave.hip) runs on a side stream beside the
+  // lanes, one wave per table's worth of LDS.
+  EncSide* side = wave_min ? enc_side() : nullptr;
+  std::unique_lock<std::mutex> lk;
+  if (wave_min) {
+    const u32 cap = max_in_len > kBlockSize ? kBlockSize : max_in_len;
+    const u32 lds = table_size_for(cap) * 2;
+    const u32 per_cu = (160u * 1024u) / (lds + 640u);  // + the static pscr / stg ring
+    const u32 waves = 256u * (per_cu ? per_cu : 1u);
+    hipStream_t wstream = stream;
+    if (side) {
+      lk = std::unique_lock<std::mutex>(side->mu);
+      if ((e = hipEventRecord(side->fork, stream)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(side->stream, side->fork, 0)) != hipSuccess) return e;
+      wstream = side->stream;
+    }
+    encode_wave_kernel<<<waves, 64, lds, wstream>>>(in, in_off, in_len, n_msgs, out, out_off, out_len, status, ctr,
+                                                   items, sizes, region_cap, kShare, kAllBytes);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (side && (e = hipEventRecord(side->join, side->stream)) != hipSuccess) return e;
+  }
+  pipe<<<slots / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off, out_len, status, tables, entries,
+                                      ctr, items, sizes, 0u, region_cap, wave_min, kShare, kAllBytes);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (items) {
+  if (side && (e = hipStreamWaitEvent(stream, side->join, 0)) != hipSuccess) return e;
+  if (lk.owns_lock()) lk.unlock();
+  if (items && can_split) {
     encode_gather_kernel<<<1024, 256, 0, stream>>>(in_len, out, out_off, out_len, status, ctr,
                                                    frag_base, big_list, sizes, region_cap);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     pipe<<<slots / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off, out_len, status,
-                                        tables, entries, ctr, nullptr, nullptr, kEncFallback, 0u);
+                                        tables, entries, ctr, nullptr, nullptr, kEncFallback, 0u, 0u, 0u, 0ull);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;

@@ -642,3 +642,66 @@ def test_decode_with_garbage_workspace(gpu, oracle, fork, fill, monkeypatch):
             assert s in (fsg.FSG_CORRUPT, fsg.FSG_BAD_HEADER), i
         else:
             assert s == fsg.FSG_OK and o[:ulen] == ref, i
+
+
+@pytest.mark.parametrize("wave_min,all_mb", [("1", "640"), ("16384", "640"), ("4096", "0")])
+def test_wave_encoder_against_oracle(gpu, oracle, wave_min, all_mb, monkeypatch):
+    """The wave encoder (hash table in LDS, one wave per fragment:
+    csrc/snappy_encode_wave.hip) takes every fragment of a split message and
+    the messages of >= FSG_ENCODE_WAVE_MIN bytes, the lane encoder the rest.
+    Bytes equal the oracle's on the golden inputs, random alphabets (runs,
+    long matches, incompressible stretches), text with random stretches,
+    periodic data, split messages (incl. capped staging regions, which force
+    the whole-message fallback) and messages of every size class.
+    FSG_ENCODE_WAVE_ALL_MB=0 gives the lanes their share of the long units
+    too (the split the encoder uses for batches of more than 640 MB of them)."""
+    monkeypatch.setenv("FSG_ENCODE_WAVE_MIN", wave_min)
+    monkeypatch.setenv("FSG_ENCODE_WAVE_ALL_MB", all_mb)
+    vecs = json.loads((GOLDEN / "vectors.json").read_text())
+    items = [build_input(v) for v in vecs]
+    rng = np.random.default_rng(int(wave_min) + 11)
+    for t in range(300):
+        n = int(rng.choice([rng.integers(0, 100), rng.integers(0, 5000), rng.integers(0, 140000)]))
+        alpha = int(rng.choice([2, 3, 8, 40, 256]))
+        items.append(rng.integers(0, alpha, n, dtype=np.uint8).tobytes())
+    for per in range(1, 70, 5):
+        items.append(bytes(((np.arange(20000 + 37 * per) % per) * 7 + 1).astype(np.uint8)))
+    for k in range(8):
+        t = bytearray(fsg.make_batch(fsg.KIND_TEXT, [40000], first_index=900 + k).item(0))
+        r = fsg.make_batch(fsg.KIND_RANDOM, [500 + 2000 * k], first_index=950 + k).item(0)
+        pos = int(rng.integers(0, len(t)))
+        items.append(bytes(t[:pos]) + r + bytes(t[pos:]))
+    for i, n in enumerate([65535, 65536, 65537, 131073, 200000, 1 << 20, 70000]):
+        kind = fsg.KIND_RANDOM if i % 3 == 1 else fsg.KIND_TEXT
+        items.append(fsg.make_batch(kind, [n], first_index=300 + i).item(0))
+    items.append(bytes(70000))  # one long run: matches far past the 20 preloaded bytes
+    comps, st = gpu.compress(fsg.Batch.from_list(items))
+    assert (st == 0).all()
+    for i, (x, c) in enumerate(zip(items, comps)):
+        assert c == oracle.compress(x), (i, len(x))
+    for cap in (4096, 40000):  # split fragments overflowing their regions
+        gpu.codec.set_split_region_cap(cap)
+        try:
+            big = [fsg.make_batch(fsg.KIND_RANDOM, [200000], first_index=7).item(0),
+                   fsg.make_batch(fsg.KIND_TEXT, [300001], first_index=8).item(0)]
+            comps, st = gpu.compress(fsg.Batch.from_list(big))
+        finally:
+            gpu.codec.set_split_region_cap(0)
+        assert (st == 0).all()
+        assert all(c == oracle.compress(x) for x, c in zip(big, comps))
+
+
+@pytest.mark.parametrize("name", ["C3", "C5"])
+def test_wave_encoder_config_digests(gpu, name, monkeypatch):
+    """Config digests (reference-generated) with the wave encoder on every
+    message of >= 16 KiB and every split fragment."""
+    monkeypatch.setenv("FSG_ENCODE_WAVE_MIN", "16384")
+    d = np.load(GOLDEN / f"digests_{name}.npz")
+    n = len(d["input_len"])
+    kind = {"C3": fsg.KIND_TEXT, "C5": fsg.KIND_PROTO}[name]
+    sizes = {"C3": np.full(n, 65536), "C5": fsg.mixed_sizes(n)}[name]
+    b = fsg.make_batch(kind, sizes)
+    comps, st = gpu.compress(b)
+    assert (st == 0).all()
+    assert np.array_equal(np.array([len(c) for c in comps], np.uint32), d["compressed_len"])
+    assert np.array_equal(np.array([fsg.fnv1a64(c) for c in comps], np.uint64), d["compressed_fnv"])
