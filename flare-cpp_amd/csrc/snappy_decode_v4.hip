@@ -2248,6 +2248,16 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   const u64 est_total_in = cap_words > 4ull * n_msgs + 64 ? (cap_words - 4ull * n_msgs - 64) * 32 : 0;
   u64 thr = 4 * est_total_in / n_msgs;
   thr = thr < kBigIndexMin ? kBigIndexMin : (thr > kBigIndexMax ? kBigIndexMax : thr);
+  // A batch of at most one wave of messages (the host runtime's one-caller
+  // batches): the lane walk would be one lane per message, its latency the
+  // longest message's tag chain (~160 us for a 4 KiB text body), where pass
+  // 1b walks each message with a whole wave (a few us).  Every message goes
+  // to pass 1b (FSG_SMALL_BATCH sets the bound; 0 disables).
+  static const u32 kSmallBatch = [] {
+    const char* e = getenv("FSG_SMALL_BATCH");
+    return e ? (u32)atoi(e) : 64u;
+  }();
+  if (n_msgs <= kSmallBatch) thr = 0;
   const u32 big_threshold = (u32)thr;
   const u32 idx_blocks = (n_msgs + 64 * kIdxWaves - 1) / (64 * kIdxWaves);
   auto launch_index = [&](bool planned) -> hipError_t {

@@ -100,6 +100,19 @@ __device__ __forceinline__ u32 eq_prefix20(const W5& a, const W5& b) {
   return n;
 }
 
+// Inclusive prefix sum over the 64 lanes (DPP row shifts and broadcasts).
+__device__ __forceinline__ u32 incl_scan64(u32 v) {
+  u32 r = v;
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xf, 0xf, true);   // row_shr:3
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x114, 0xf, 0xe, false);  // row_shr:4, banks 1-3
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x118, 0xf, 0xc, false);  // row_shr:8, banks 2-3
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  r += (u32)__builtin_amdgcn_update_dpp(0, (int)r, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return r;
+}
+
 // Byte-exact store of the low nb (1..4) bytes of v (one lane).
 __device__ __forceinline__ void st_bytes(u8* p, u32 v, u32 nb) {
   if (nb == 4) {
@@ -230,6 +243,49 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
     }
     const u32 t = copy_tag(offset, len, &nb);
     put_tag(t, nb);
+  };
+
+  // ---- deferred emission: the block's common events (a literal whose bytes
+  // are in this block's or the previous block's registers, a copy of <= 64
+  // bytes) are recorded one per lane (lane nev: q | literal length << 16,
+  // candidate | match length << 16) and written together: sizes, a prefix
+  // sum, then one output byte per lane.  Other events flush the recorded ones
+  // first and take the paths above.
+  u32 EQL = 0, ECM = 0, nev = 0;
+  auto emit_pending = [&](u32 B, u32 xw0c, u32 xw0p) -> bool {
+    if (!nev) return true;
+    const u32 q = EQL & 0xffffu, L = EQL >> 16, cand = ECM & 0xffffu, ml = ECM >> 16;
+    const bool ve = lane < nev;
+    const u32 nm1 = L - 1;
+    const u32 tl = L == 0 ? 0u : (nm1 < 60 ? 1u : 2u);  // L <= 128 here
+    const u32 lt = nm1 < 60 ? nm1 << 2 : (240u | (nm1 << 8));
+    u32 cnb;
+    const u32 ct = copy_tag(q - cand, ml, &cnb);
+    const u32 sz = ve ? tl + L + cnb : 0u;
+    const u32 incl = incl_scan64(sz);
+    const u32 excl = incl - sz;
+    const u32 total = rl(incl, 63);
+    if (!room(total)) return false;
+    // per event: output offset, literal tag length, literal length, literal
+    // start relative to B - 64 (0..127)
+    const u32 A = excl | (tl << 12) | (L << 14) | ((q - L - (B - 64)) << 22);
+    for (u32 j0 = 0; j0 < total; j0 += 64) {
+      const u32 j = j0 + lane;
+      u32 e = 0;
+      for (u32 k = 1; k < nev; ++k) e = j >= rl(excl, k) ? k : e;
+      const u32 a = bperm(A, e), ltv = bperm(lt, e), ctv = bperm(ct, e);
+      const u32 r = j - (a & 0xfffu), tle = (a >> 12) & 3u, le = (a >> 14) & 0xffu, xs = a >> 22;
+      const u32 x = xs + (r - tle);  // literal byte's position relative to B - 64
+      const u32 bp = bperm(xw0p, x & 63), bc = bperm(xw0c, x & 63);
+      u32 byte;
+      if (r < tle) byte = ltv >> (8 * r);
+      else if (r < tle + le) byte = x < 64 ? bp : bc;
+      else byte = ctv >> (8 * ((r - tle - le) & 3));
+      if (j < total) stg[(opos + j) & 511] = (u8)byte;
+    }
+    opos += total;
+    nev = 0;
+    return true;
   };
 
   u32 next_emit = 0;
@@ -463,10 +519,8 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
           I |= S & (ks == 63 ? ~0ull : ((2ull << ks) - 1));
           q = B + ks;
           STAMP(3);
-          // literal [next_emit, q) (snappy.cc:403)
-          if (!room(q - next_emit + 5)) return nullptr;
-          emit_literal(next_emit, q, B, X, prev_ok, xwp.w[0]);
         }
+        // literal [next_emit, q) (snappy.cc:403; empty after a copy)
         // ---- copy at q (FindMatchLength, snappy-internal.h:87-121)
         const u32 cand = pk & 0xffffu;
         u32 mlen = (pk >> 16) & 31u;
@@ -498,8 +552,24 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
           STAMP(7);
         }
         if (mlen > n - q) mlen = n - q;
-        if (!room(3 * (mlen / 60 + 2))) return nullptr;
-        emit_copy(q - cand, mlen);
+        {
+          const u32 L = q - next_emit;
+          const bool lit_regs = L == 0 || next_emit >= B || (prev_ok && next_emit + 64 >= B);
+          if (lit_regs && mlen <= 64) {
+            const bool mine = lane == nev;
+            EQL = mine ? q | (L << 16) : EQL;
+            ECM = mine ? cand | (mlen << 16) : ECM;
+            ++nev;
+          } else {
+            if (!emit_pending(B, X, xwp.w[0])) return nullptr;
+            if (L) {
+              if (!room(L + 5)) return nullptr;
+              emit_literal(next_emit, q, B, X, prev_ok, xwp.w[0]);
+            }
+            if (!room(3 * (mlen / 60 + 2))) return nullptr;
+            emit_copy(q - cand, mlen);
+          }
+        }
         ip = q + mlen;
         next_emit = ip;
         if (ip >= lim) { done = true; break; }
@@ -515,6 +585,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       lds_fence();
       if ((I >> lane) & 1ull) table[h] = (u16)(B + lane);
       lds_fence();
+      if (!emit_pending(B, X, xwp.w[0])) return nullptr;
       pend_end = opos;
       STAMP(5);
       if (done) break;

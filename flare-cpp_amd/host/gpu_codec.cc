@@ -408,11 +408,17 @@ bool Device::run(const std::vector<Request*>& reqs, Kind kind, Counters* ctr) {
            hipMemcpyAsync(dg_len + ja, g_len + ja, 4ull * jn, hipMemcpyHostToDevice, st) == hipSuccess &&
            fsg_gather_blocks(dg_src + ja, dg_len + ja, dg_dst + ja, jn, d_in.as<uint8_t>(), st) == FSG_SUCCESS;
     }
-    // this chunk's offsets, lengths and caps (four column slices)
-    ok = ok && hipMemcpyAsync(d_in_off + a, in_off + a, 8ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
-    ok = ok && hipMemcpyAsync(d_out_off + a, out_off + a, 8ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
-    ok = ok && hipMemcpyAsync(d_in_len + a, in_len + a, 4ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
-    ok = ok && hipMemcpyAsync(d_out_cap + a, out_cap + a, 4ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
+    // this chunk's offsets, lengths and caps: four column slices, or (one
+    // chunk: the whole batch) the four columns in one copy -- per-copy
+    // latency dominates a small batch
+    if (n_chunks == 1) {
+      ok = ok && hipMemcpyAsync(d_in_off, in_off, 24ull * n, hipMemcpyHostToDevice, st) == hipSuccess;
+    } else {
+      ok = ok && hipMemcpyAsync(d_in_off + a, in_off + a, 8ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
+      ok = ok && hipMemcpyAsync(d_out_off + a, out_off + a, 8ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
+      ok = ok && hipMemcpyAsync(d_in_len + a, in_len + a, 4ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
+      ok = ok && hipMemcpyAsync(d_out_cap + a, out_cap + a, 4ull * cn, hipMemcpyHostToDevice, st) == hipSuccess;
+    }
     if (!ok) {
       fprintf(stderr, "[flare-snappy-gpu] H2D copy failed on device %d\n", id);
       failed = true;
@@ -441,8 +447,10 @@ bool Device::run(const std::vector<Request*>& reqs, Kind kind, Counters* ctr) {
       failed = true;
       break;
     }
-    ok = hipMemcpyAsync(out_len + a, d_out_len + a, 4ull * cn, hipMemcpyDeviceToHost, st) == hipSuccess &&
-         hipMemcpyAsync(status + a, d_status + a, 4ull * cn, hipMemcpyDeviceToHost, st) == hipSuccess &&
+    ok = (n_chunks == 1
+              ? hipMemcpyAsync(out_len, d_out_len, 8ull * n, hipMemcpyDeviceToHost, st) == hipSuccess
+              : hipMemcpyAsync(out_len + a, d_out_len + a, 4ull * cn, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                    hipMemcpyAsync(status + a, d_status + a, 4ull * cn, hipMemcpyDeviceToHost, st) == hipSuccess) &&
          (validate || ob == oa ||
           hipMemcpyAsync(hout + oa, d_out.as<uint8_t>() + oa, ob - oa, hipMemcpyDeviceToHost, st) == hipSuccess);
     if (!ok) {

@@ -11,6 +11,7 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parents[1]
 os.environ["FSG_LIB"] = str(REPO / "flare-cpp_amd" / "lib" / "libflare_snappy_gpu_stamps.so")
 os.environ["FSG_ENCODE_WAVE_MIN"] = os.environ.get("FSG_ENCODE_WAVE_MIN", "1")
+os.environ["FSG_ENCODE_WAVE_ALL_MB"] = os.environ.get("FSG_ENCODE_WAVE_ALL_MB", "100000")  # every unit on the wave encoder
 sys.path.insert(0, str(REPO / "flare-cpp_amd" / "py"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
