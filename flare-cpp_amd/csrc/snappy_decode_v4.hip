@@ -1425,6 +1425,7 @@ __device__ __forceinline__ void exec_message(
       wait_all_memory();
 #endif
       const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
+#ifndef FSG_KO_SLIDE
       for (u32 k = 0; k < keep; k += 1024) {
         const u32 i = k + 16 * lane;
         u32x4 x = u32x4{0, 0, 0, 0};
@@ -1433,6 +1434,9 @@ __device__ __forceinline__ void exec_message(
         if (i < keep) *reinterpret_cast<u32x4*>(sb + i) = x;
         wave_lds_fence();
       }
+#else
+      (void)shift;
+#endif
       sbase = nsb;
       zero_end = (keep + 15) & ~15u;  // the copied blocks end in zeros past op
     }
@@ -1654,6 +1658,7 @@ __device__ __forceinline__ void exec5_message(
 
   auto flush_to = [&](u32 fe) {
     if (fe <= flushed) return;
+#ifndef FSG_KO_FLUSH  // knockout builds (diagnostic, wrong output): time shares
     const int b0 = (int)(((flushed + obal) & ~15u)) - (int)obal;
     for (int blk = b0 + 16 * (int)lane; blk < (int)fe; blk += 1024) {
       const u32 lo = blk < (int)flushed ? flushed : (u32)blk;
@@ -1665,6 +1670,7 @@ __device__ __forceinline__ void exec5_message(
         store_exact(ob + lo, lds_read16(sb + ((int)lo - sbase)), hi - lo);
       }
     }
+#endif
     flushed = fe;
   };
 
@@ -1787,6 +1793,7 @@ __device__ __forceinline__ void exec5_message(
       if ((int)flushed < nsb + 16) flush_to((u32)((int)((op + obal) & ~15u) - (int)obal));
       wait_all_memory();
       const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
+#ifndef FSG_KO_SLIDE
       for (u32 k = 0; k < keep; k += 1024) {
         const u32 i = k + 16 * lane;
         u32x4 x = u32x4{0, 0, 0, 0};
@@ -1795,6 +1802,9 @@ __device__ __forceinline__ void exec5_message(
         if (i < keep) *reinterpret_cast<u32x4*>(sb + i) = x;
         wave_lds_fence();
       }
+#else
+      (void)shift;
+#endif
       sbase = nsb;
       zero_end = (keep + 15) & ~15u;
     }
@@ -1808,7 +1818,9 @@ __device__ __forceinline__ void exec5_message(
       pf_cnt = ncnt;
     }
     while (op + tot_len + 20 - sbase > zero_end) {
+#ifndef FSG_KO_ZERO
       zero_from(zero_end);
+#endif
       zero_end += 1024;
     }
     wave_lds_fence();
@@ -1848,9 +1860,13 @@ __device__ __forceinline__ void exec5_message(
     };
     u32x4 a0 = xr, a1 = u32x4{0, 0, 0, 0};
     u32 a0e = 0, a1e = 0;
+#ifndef FSG_KO_LOADS
     if (kf > 0 && !reg0) gload(0, a0, a0e);
+#endif
     const u64 m1 = __ballot(kf > 1);
+#ifndef FSG_KO_LOADS
     if (m1 && kf > 1) gload(1, a1, a1e);
+#endif
     if (prio) __builtin_amdgcn_s_setprio(0);
     STAMP(3);
     {  // the previous groups' completed blocks, while the loads are in flight
@@ -1859,8 +1875,12 @@ __device__ __forceinline__ void exec5_message(
     }
     STAMP(4);
     const u32 wa = (u32)((int)t_op - sbase);
+#ifdef FSG_KO_A
+    if (m1 && false) {
+#else
     if (kf > 0) or_store(sb, wa, shf(a0, a0e, reg0 ? 0u : sh), len < 16 ? len : 16u, mtab);
     if (m1) {
+#endif
       if (kf > 1) or_store(sb, wa + 16, shf(a1, a1e, sh), len - 16 < 16 ? len - 16 : 16u, mtab);
       // chunks 2-3 (literals and far copies of 33..64 bytes: rare) reuse the
       // registers, one more round trip
