@@ -1067,6 +1067,476 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
 }
 
 // ===========================================================================
+// Pass 1b, chunked (the huge messages of the forked path): one wave walking a
+// ~520 KB body serially was CM's longest chain (5.6 ms).  The body's
+// compressed bytes are cut into kChunkBytes chunks, walked in parallel:
+//
+//   spec   one wave per chunk walks from the chunk's first byte AS IF a tag
+//          started there (chunk 0: from the header's end, exact) and writes
+//          that chain's tag-start bits for the chunk, its exit (the first chain
+//          position past the chunk), the output length of its tags and whether
+//          it reached a tag that cannot be decoded.
+//   fixup  one wave per message, chunk by chunk: the true chain enters chunk k
+//          at chunk k-1's true exit; it is followed (pointer doubling, a window
+//          at a time) until it reaches a tag start of the speculative chain --
+//          from there both chains are one chain, so chunk k's speculative bits,
+//          exit and length hold (text meets within ~10 bytes).
+//          The bits before the meeting point are rewritten, the chunk's true
+//          output length corrected, and the chunks' output bases summed.  A
+//          chunk the true chain crosses without meeting is rewritten whole.
+//   check  one wave per chunk, with the true bits and base: the writer checks
+//          (snappy.cc:1166, :1200, :1400, :1410, :1466) and the 64 KiB segment
+//          rules of index_big_message.
+//   final  one wave per message: status and pass 2's work lists.
+// ===========================================================================
+constexpr u32 kChunkBytes = 32 * 1024;  // a multiple of 512: chunks own whole bitmap words
+struct ChunkRec {
+  u32 m, k, exit, bad, len, base, flags, nchunks;
+};
+constexpr u32 kChunkBad = 1, kChunkNoSeg = 2;
+
+namespace {
+// The candidate tag at message position p (stage st holds positions
+// [spos, spos + kBigStageBytes)): pass 1b's branch-free decode.
+struct Cand2 {
+  u32 len, coff, nxt, J;
+  bool lit, bad_local;
+};
+__device__ __forceinline__ Cand2 decode_cand(const u32* st, int spos, u32 p, u32 n_in, u32 lane) {
+  const u32 s = p - (u32)spos;
+  const u32 dw = s >> 2, bsh = s & 3;
+  const u32 lo = st[dw], hi = st[dw + 1];
+  const u32 t0 = alignbyte(hi, lo, bsh);
+  const u32 b4 = (hi >> (8 * bsh)) & 0xffu;
+  const u32 c = t0 & 0xffu;
+  const u32 type = c & 3;
+  Cand2 d;
+  d.lit = type == 0;
+  const u32 l0 = (c >> 2) + 1;
+  const bool longlit = d.lit & (l0 >= 61);
+  const u32 nb = d.lit ? (longlit ? l0 - 60 : 0u) : (1u << (type - 1));
+  const u32 ext = (b4 << 24) | (t0 >> 8);
+  const u32 val = nb >= 4 ? ext : ext & ((1u << (8 * nb)) - 1u);
+  d.len = d.lit ? (longlit ? val + 1u : l0) : (type == 1 ? 4 + ((c >> 2) & 7) : l0);
+  d.coff = type == 1 ? (((c >> 5) << 8) | val) : val;
+  const u32 avail = n_in - p - 1;
+  d.bad_local = (p >= n_in) | (avail < nb) | (d.lit & (avail - nb < d.len));
+  const u32 adv = 1 + nb + (d.lit ? d.len : 0u);
+  d.nxt = p + adv;
+  d.J = (d.bad_local || adv >= 64 - lane || d.nxt >= n_in) ? 64u : lane + adv;
+  return d;
+}
+
+// Stage input covering [wb, wb + 72) for the window at wb (kept across calls).
+struct Stage {
+  int spos = -1;
+  u32 send = 0;
+};
+__device__ __forceinline__ void stage_for(Stage& sg, u32* st, const u8* abase, u32 ibal, u32 last_chunk, u32 wb,
+                                          u32 lane) {
+  if (sg.spos >= 0 && wb >= (u32)sg.spos && wb + 72 <= sg.send) return;
+  const u32 c0 = (wb + ibal) >> 4;
+  u32x4 x[kBigStageChunks / 64];
+#pragma unroll
+  for (u32 r = 0; r < kBigStageChunks / 64; ++r) {
+    u32 k = c0 + r * 64 + lane;
+    k = k <= last_chunk ? k : last_chunk;
+    x[r] = *reinterpret_cast<const u32x4*>(abase + 16 * k);
+  }
+  wave_lds_fence();
+#pragma unroll
+  for (u32 r = 0; r < kBigStageChunks / 64; ++r) *reinterpret_cast<u32x4*>(st + 4 * (r * 64 + lane)) = x[r];
+  wave_lds_fence();
+  sg.spos = (int)(16 * c0) - (int)ibal;
+  sg.send = (u32)sg.spos + kBigStageBytes - 8;
+}
+
+// The chain from position `first` inside the window at wb (pointer doubling
+// over the lanes' successors, as index_big_message): bit j = a tag starts at
+// wb + j on that chain.
+__device__ __forceinline__ u64 window_chain(const Cand2& d, u32 first, u32 lane) {
+  u32 J = d.J;
+  u64 M = 1ull << lane;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const u32 src = J < 64 ? J : lane;
+    const u64 Mj = ((u64)(u32)__shfl((int)(u32)(M >> 32), (int)src, 64) << 32) | (u32)__shfl((int)(u32)M, (int)src, 64);
+    const u32 Jj = (u32)__shfl((int)J, (int)src, 64);
+    if (J < 64) {
+      M |= Mj;
+      J = Jj;
+    }
+  }
+  return ((u64)readlane((u32)(M >> 32), first) << 32) | readlane((u32)M, first);
+}
+
+__device__ __forceinline__ u64 bm_window(const u32* bm, u32 wb) {
+  return ((u64)bm[(wb >> 5) + 1] << 32) | bm[wb >> 5];
+}
+// positions [lo, hi) of the window at wb as a mask
+__device__ __forceinline__ u64 range_mask(u32 wb, u32 lo, u32 hi) {
+  const u32 a = lo > wb ? lo - wb : 0u, b = hi > wb ? (hi - wb < 64 ? hi - wb : 64u) : 0u;
+  if (a >= b) return 0ull;
+  const u64 up = b >= 64 ? ~0ull : ((1ull << b) - 1);
+  return up & ~((1ull << a) - 1);
+}
+}  // namespace
+
+// The chunk records of the huge messages (set 1 of the forked path): one
+// thread per huge message (listed from the end of big_list).
+__global__ void chunk_list_kernel(const u8* __restrict__ in, const u64* __restrict__ in_off,
+                                  const u32* __restrict__ in_len, const u32* __restrict__ big_count,
+                                  const u32* __restrict__ big_list, u32 n_msgs, u32 flags,
+                                  u32* __restrict__ chunk_count, ChunkRec* __restrict__ recs,
+                                  u32* __restrict__ first_rec, u32 max_recs) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 n_huge = big_count[8];
+  if (i >= n_huge) return;
+  const u32 m = big_list[n_msgs - 1 - i];
+  const u32 n_in = in_len[m];
+  const u32 K = (n_in + kChunkBytes - 1) / kChunkBytes;
+  const u32 b = atomicAdd(chunk_count, K);
+  first_rec[i] = b + K <= max_recs ? b : 0xffffffffu;
+  if (b + K > max_recs) return;
+  for (u32 k = 0; k < K; ++k) {
+    ChunkRec r{};
+    r.m = m;
+    r.k = k;
+    r.nchunks = K;
+    recs[b + k] = r;
+  }
+  (void)in;
+  (void)in_off;
+  (void)flags;
+}
+
+// spec: one wave per chunk record (work counter).
+__global__ __launch_bounds__(4 * 64) void chunk_spec_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u32 flags,
+    const u32* __restrict__ bm_base, u32* __restrict__ bitmap, const u32* __restrict__ chunk_count,
+    ChunkRec* __restrict__ recs, u32* __restrict__ next, u32 max_recs) {
+  __shared__ u32 stage_s[4][kBigStageBytes / 4 + 4];
+  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const u32 lane = threadIdx.x & 63;
+  const u32 cnt = *chunk_count < max_recs ? *chunk_count : max_recs;
+  u32* st = stage_s[wv];
+  for (;;) {
+    const u32 got = atomicAdd(next, lane == 0 ? 1u : 0u);
+    const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
+    if (idx >= cnt) break;
+    const ChunkRec r = recs[idx];
+    const u32 m = (u32)__builtin_amdgcn_readfirstlane((int)r.m);
+    const u8* ib = in + in_off[m];
+    const u32 n_in = in_len[m];
+    const u32 cs = r.k * kChunkBytes;
+    const u32 ce = cs + kChunkBytes < n_in ? cs + kChunkBytes : n_in;
+    u32* bm = bitmap + bm_base[m];
+    // this chunk's bitmap words (the last chunk: up to the allocation's end)
+    {
+      const u32 w0 = cs >> 5;
+      const u32 w1 = ce == n_in ? ((((n_in + 31) >> 5) + 3) & ~3u) : ce >> 5;
+      for (u32 wd = w0 + lane; wd < w1; wd += 64) bm[wd] = 0u;
+    }
+    u32 ip = cs;
+    if (r.k == 0) {
+      u32 ulen = 0;
+      ip = (u32)parse_varint_header(ib, n_in, flags & 2u, &ulen);
+    }
+    const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
+    const u8* abase = ib - ibal;
+    const u32 last_chunk = (ibal + n_in - 1) >> 4;
+    Stage sg;
+    u32 op = 0, bad = 0;
+    wave_lds_fence();
+    for (u32 guard = 0; guard < kChunkBytes + 64; ++guard) {
+      if (ip >= ce || ip >= n_in) break;
+      const u32 wb = ip & ~31u;
+      stage_for(sg, st, abase, ibal, last_chunk, wb, lane);
+      const Cand2 d = decode_cand(st, sg.spos, wb + lane, n_in, lane);
+      const u64 S = window_chain(d, ip - wb, lane);
+      const u64 Sin = S & range_mask(wb, cs, ce);
+      const bool in_s = (Sin >> lane) & 1ull;
+      if (__any(in_s && d.bad_local)) {
+        bad = 1;
+        // the chain stops at its first undecodable tag
+        const u64 B = __ballot(in_s && d.bad_local);
+        ip = wb + (u32)__builtin_ctzll(B);
+        const u64 keep = Sin & ((1ull << (ip - wb)) | ((1ull << (ip - wb)) - 1));
+        if (lane < 2) {
+          const u32 wbits = lane == 0 ? (u32)keep : (u32)(keep >> 32);
+          if (wbits) atomicOr(bm + (wb >> 5) + lane, wbits);
+        }
+        break;
+      }
+      const u32 lv = in_s ? d.len : 0u;
+      op += readlane(dpp_incl_scan(lv), 63);
+      if (lane < 2) {
+        const u32 wbits = lane == 0 ? (u32)Sin : (u32)(Sin >> 32);
+        if (wbits) atomicOr(bm + (wb >> 5) + lane, wbits);
+      }
+      const u32 last = 63u - (u32)__builtin_clzll(S);
+      ip = readlane(d.nxt, last);
+    }
+    if (lane == 0) {
+      recs[idx].exit = ip;
+      recs[idx].bad = bad;
+      recs[idx].len = op;
+    }
+  }
+}
+
+// fixup: one wave per huge message, chunk by chunk (see above).  mstat[i]:
+// 1 = the message's chain is sound end to end (its chunks' checks follow).
+__global__ __launch_bounds__(4 * 64) void chunk_fixup_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len,
+    const u32* __restrict__ out_len, const u32* __restrict__ bm_base, u32* __restrict__ bitmap,
+    const u32* __restrict__ big_count, ChunkRec* __restrict__ recs, const u32* __restrict__ first_rec,
+    u32* __restrict__ mstat, u32* __restrict__ next) {
+  __shared__ u32 stage_s[4][kBigStageBytes / 4 + 4];
+  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const u32 lane = threadIdx.x & 63;
+  const u32 n_huge = big_count[8];
+  u32* st = stage_s[wv];
+  for (;;) {
+    const u32 got = atomicAdd(next, lane == 0 ? 1u : 0u);
+    const u32 i = (u32)__builtin_amdgcn_readfirstlane((int)got);
+    if (i >= n_huge) break;
+    const u32 b = first_rec[i];
+    if (b == 0xffffffffu) continue;  // (records did not fit: cannot happen with the sized workspace)
+    const u32 m = (u32)__builtin_amdgcn_readfirstlane((int)recs[b].m);
+    const u32 K = recs[b].nchunks;
+    const u8* ib = in + in_off[m];
+    const u32 n_in = in_len[m];
+    const u32 expected = out_len[m];
+    u32* bm = bitmap + bm_base[m];
+    const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
+    const u8* abase = ib - ibal;
+    const u32 last_chunk = (ibal + n_in - 1) >> 4;
+    Stage sg;
+    bool ok = recs[b].bad == 0;
+    u32 e = recs[b].exit, run = recs[b].len;
+    if (lane == 0) recs[b].base = 0;
+    // the lengths of the tags in `mask` of the window at wb (all lanes)
+    auto mask_len = [&](u32 wb, u64 mask, const Cand2& d) -> u32 {
+      const bool in_m = (mask >> lane) & 1ull;
+      return readlane(dpp_incl_scan(in_m ? d.len : 0u), 63);
+    };
+    for (u32 k = 1; k < K && ok; ++k) {
+      const u32 cs = k * kChunkBytes;
+      const u32 ce = cs + kChunkBytes < n_in ? cs + kChunkBytes : n_in;
+      const ChunkRec R = recs[b + k];
+      if (lane == 0) recs[b + k].base = run;
+      const u32 w0 = cs >> 5;
+      const u32 w1 = ce == n_in ? ((((n_in + 31) >> 5) + 3) & ~3u) : ce >> 5;
+      if (e >= ce) {  // a literal spans the chunk: no tag starts in it
+        wave_lds_fence();
+        for (u32 wd = w0 + lane; wd < w1; wd += 64) bm[wd] = 0u;
+        if (lane == 0) recs[b + k].len = 0;
+        continue;
+      }
+      // ---- the true chain from e until it meets a speculative tag start
+      u32 pos = e, true_len = 0, meet = 0xffffffffu;
+      for (u32 guard = 0; guard < kChunkBytes; ++guard) {
+        if (pos >= ce) break;
+        const u32 wb = pos & ~31u;
+        stage_for(sg, st, abase, ibal, last_chunk, wb, lane);
+        const Cand2 d = decode_cand(st, sg.spos, wb + lane, n_in, lane);
+        const u64 S = window_chain(d, pos - wb, lane);
+        const u64 Sin = S & range_mask(wb, cs, ce);
+        const u64 SP = bm_window(bm, wb) & range_mask(wb, cs, ce);
+        const u64 common = Sin & SP;
+        u64 T = Sin;
+        if (common) {
+          meet = wb + (u32)__builtin_ctzll(common);
+          T = Sin & ((1ull << (meet - wb)) - 1);
+        }
+        if (__any(((T >> lane) & 1ull) && d.bad_local)) {
+          ok = false;
+          break;
+        }
+        true_len += mask_len(wb, T, d);
+        if (meet != 0xffffffffu) break;
+        const u32 last = 63u - (u32)__builtin_clzll(S);
+        pos = readlane(d.nxt, last);
+      }
+      if (!ok) break;
+      u32 spec_before = 0;
+      if (meet != 0xffffffffu) {
+        // the speculative tags in [cs, meet): their output length
+        for (u32 wb = cs; wb < meet; wb += 64) {
+          const u64 SP = bm_window(bm, wb) & range_mask(wb, cs, meet);
+          if (!SP) continue;
+          stage_for(sg, st, abase, ibal, last_chunk, wb, lane);
+          const Cand2 d = decode_cand(st, sg.spos, wb + lane, n_in, lane);
+          spec_before += mask_len(wb, SP, d);
+        }
+        if (R.bad) ok = false;  // the true chain runs into the speculative chain's bad tag
+      }
+      // ---- rewrite the bits before the meeting point (the whole chunk if
+      // none): clear them, then walk the true chain from e again, setting its
+      const u32 upto = meet != 0xffffffffu ? meet : ce;
+      wave_lds_fence();
+      for (u32 wd = w0 + lane; wd < ((upto + 31) >> 5); wd += 64) {
+        const u32 lo = wd << 5;
+        const u32 keepm = upto >= lo + 32 ? 0u : (0xffffffffu << (upto - lo));  // bits from the meet on stay
+        bm[wd] &= keepm;
+      }
+      if (meet == 0xffffffffu && ce == n_in)
+        for (u32 wd = ((ce + 31) >> 5) + lane; wd < w1; wd += 64) bm[wd] = 0u;
+      wave_lds_fence();
+      {
+        u32 p2 = e;
+        for (u32 guard = 0; guard < kChunkBytes && p2 < upto; ++guard) {
+          const u32 wb = p2 & ~31u;
+          stage_for(sg, st, abase, ibal, last_chunk, wb, lane);
+          const Cand2 d = decode_cand(st, sg.spos, wb + lane, n_in, lane);
+          const u64 S = window_chain(d, p2 - wb, lane);
+          const u64 T = S & range_mask(wb, cs, upto);
+          if (lane < 2) {
+            const u32 wbits = lane == 0 ? (u32)T : (u32)(T >> 32);
+            if (wbits) bm[(wb >> 5) + lane] |= wbits;
+          }
+          const u32 last = 63u - (u32)__builtin_clzll(S);
+          p2 = readlane(d.nxt, last);
+        }
+      }
+      const u32 new_len = meet != 0xffffffffu ? true_len + R.len - spec_before : true_len;
+      if (lane == 0) recs[b + k].len = new_len;
+      run += new_len;
+      e = meet != 0xffffffffu ? R.exit : pos;
+    }
+    if (ok) ok = e == n_in && run == expected;
+    if (lane == 0) mstat[i] = ok ? 1u : 0u;
+  }
+}
+
+// check: one wave per chunk record, with the true bits and the chunk's base.
+__global__ __launch_bounds__(4 * 64) void chunk_check_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len,
+    const u32* __restrict__ out_len, const u32* __restrict__ bm_base, const u32* __restrict__ bitmap,
+    const u32* __restrict__ chunk_count, ChunkRec* __restrict__ recs, u8* out, const u64* __restrict__ out_off,
+    u32* __restrict__ next, u32 max_recs) {
+  __shared__ u32 stage_s[4][kBigStageBytes / 4 + 4];
+  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const u32 lane = threadIdx.x & 63;
+  const u32 cnt = *chunk_count < max_recs ? *chunk_count : max_recs;
+  u32* st = stage_s[wv];
+  for (;;) {
+    const u32 got = atomicAdd(next, lane == 0 ? 1u : 0u);
+    const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
+    if (idx >= cnt) break;
+    const ChunkRec R = recs[idx];
+    const u32 m = (u32)__builtin_amdgcn_readfirstlane((int)R.m);
+    const u8* ib = in + in_off[m];
+    u8* ob = out + out_off[m];
+    const u32 n_in = in_len[m];
+    const u32 expected = out_len[m];
+    const u32* bm = bitmap + bm_base[m];
+    const u32 cs = R.k * kChunkBytes;
+    const u32 ce = cs + kChunkBytes < n_in ? cs + kChunkBytes : n_in;
+    const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
+    const u8* abase = ib - ibal;
+    const u32 last_chunk = (ibal + n_in - 1) >> 4;
+    Stage sg;
+    u32 op = (u32)__builtin_amdgcn_readfirstlane((int)R.base), flags = 0;
+    for (u32 wb = cs; wb < ce; wb += 64) {
+      const u64 S = bm_window(bm, wb) & range_mask(wb, cs, ce);
+      if (!S) continue;
+      stage_for(sg, st, abase, ibal, last_chunk, wb, lane);
+      const u32 p = wb + lane;
+      const Cand2 d = decode_cand(st, sg.spos, p, n_in, lane);
+      const bool in_s = (S >> lane) & 1ull;
+      const u32 lv = in_s ? d.len : 0u;
+      const u32 incl = dpp_incl_scan(lv);
+      const u32 t_op = op + incl - lv;
+      // writer space and copy offset checks (:761, :1166, :1200, :1410, :1466)
+      if (__any(in_s && (d.bad_local || expected - t_op < d.len || (!d.lit && d.coff - 1u >= t_op)))) flags |= kChunkBad;
+      // 64 KiB output segments (index_big_message's rules)
+      const bool span = in_s && d.len > 0 && ((t_op ^ (t_op + d.len - 1)) >> 16) != 0;
+      const bool xcopy = in_s && !d.lit && t_op - d.coff < (t_op & ~0xffffu);
+      if (__any(span || xcopy)) flags |= kChunkNoSeg;
+      if (!(flags & kChunkNoSeg) && in_s && t_op != 0 && (t_op & 0xffffu) == 0 && t_op + 4 <= expected)
+        __builtin_memcpy(ob + t_op, &p, 4);
+      op += readlane(incl, 63);
+    }
+    if (lane == 0) recs[idx].flags = flags;
+  }
+}
+
+// After pass 1b: a message's status and its place in pass 2's work lists
+// (its 64 KiB segments when the stream allows them, else the whole message).
+__device__ __forceinline__ void list_big_message(u32 m, i32 st, bool seg, u32 lane, const u32* __restrict__ out_len,
+                                                 i32* __restrict__ status_out, u32 n_msgs,
+                                                 u64* __restrict__ seg_list, u32* __restrict__ seg_count,
+                                                 u32* __restrict__ whole_list, u32* __restrict__ whole_count) {
+  if (lane == 0) status_out[m] = st;
+  if (st != kOk) return;
+  const u32 expected = out_len[m];
+  u32 nseg = 0;  // > 1: run as segments
+  if (seg && expected > 65536u) {
+    nseg = (expected + 65535u) >> 16;
+    if (expected - ((nseg - 1) << 16) < 4) --nseg;  // the tail joins the previous segment
+  }
+  bool whole = nseg < 2;
+  if (!whole) {
+    u32 b = 0;
+    if (lane == 0) b = atomicAdd(seg_count, nseg);
+    b = readlane(b, 0);
+    for (u32 k = lane; k < nseg; k += 64) {
+      const u64 e = b + k < n_msgs ? ((u64)m | ((u64)k << 32) | ((u64)(k == nseg - 1) << 63)) : 0xffffffffull;
+      if (b + k < n_msgs) seg_list[b + k] = e;
+    }
+    if (b + nseg > n_msgs) {
+      for (u32 k = lane; b + k < n_msgs && k < nseg; k += 64) seg_list[b + k] = 0xffffffffull;
+      whole = true;
+    }
+  }
+  if (whole) {
+    u32 b = 0;
+    if (lane == 0) b = atomicAdd(whole_count, 1u);
+    b = readlane(b, 0);
+    if (lane == 0) whole_list[b] = m;
+  }
+}
+
+// final: one wave per huge message (a message whose records did not fit is
+// walked here serially, as index_big_kernel would).
+__global__ __launch_bounds__(4 * 64) void chunk_final_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u32 flags,
+    const u32* __restrict__ bm_base, u32* __restrict__ bitmap, u8* out, const u64* __restrict__ out_off,
+    const u32* __restrict__ big_list, const u32* __restrict__ out_len, i32* __restrict__ status_out,
+    const u32* __restrict__ big_count, const ChunkRec* __restrict__ recs, const u32* __restrict__ first_rec,
+    const u32* __restrict__ mstat, u32 n_msgs, u64* __restrict__ seg_list, u32* __restrict__ seg_count,
+    u32* __restrict__ whole_list, u32* __restrict__ whole_count, u32* __restrict__ next) {
+  __shared__ u32 stage_s[4][kBigStageBytes / 4 + 4];
+  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const u32 lane = threadIdx.x & 63;
+  const u32 n_huge = big_count[8];
+  for (;;) {
+    const u32 got = atomicAdd(next, lane == 0 ? 1u : 0u);
+    const u32 i = (u32)__builtin_amdgcn_readfirstlane((int)got);
+    if (i >= n_huge) break;
+    const u32 b = first_rec[i];
+    if (b == 0xffffffffu) {
+      const u32 m = big_list[n_msgs - 1 - i];
+      bool seg = true;
+      const i32 st = index_big_message(m, in, in_off, in_len, out_len, flags & 2u, bm_base, bitmap, stage_s[wv],
+                                       lane, out + out_off[m], seg);
+      list_big_message(m, st, seg, lane, out_len, status_out, n_msgs, seg_list, seg_count, whole_list, whole_count);
+      continue;
+    }
+    const u32 m = (u32)__builtin_amdgcn_readfirstlane((int)recs[b].m);
+    const u32 K = recs[b].nchunks;
+    u32 fl = 0;
+    for (u32 k = lane; k < K; k += 64) fl |= recs[b + k].flags;
+    const bool bad = __any(fl & kChunkBad), noseg = __any(fl & kChunkNoSeg);
+    const bool ok = mstat[i] != 0 && !bad;
+    list_big_message(m, ok ? kOk : kCorrupt, !noseg, lane, out_len, status_out, n_msgs, seg_list, seg_count,
+                     whole_list, whole_count);
+  }
+}
+
+// ===========================================================================
 // Pass 2: execute.  One wave per status-OK message.
 //
 // Output is assembled in a per-wave LDS window `sb` (kWindow bytes) holding
@@ -2120,11 +2590,17 @@ constexpr u32 kWsSet0SegCount = 160;
 constexpr u32 kWsSet0ExecNext = 192;   // pass-2 queue head
 constexpr u32 kWsSet0WholeCount = 224;
 constexpr u32 kWsSet1ExecNext = 240;
+constexpr u32 kWsChunkCount = 80;      // chunked pass 1b: records listed
+constexpr u32 kWsChunkSpecNext = 84;   //   work counters of its passes
+constexpr u32 kWsChunkFixNext = 88;
+constexpr u32 kWsChunkCheckNext = 92;
+constexpr u32 kWsChunkFinalNext = 100;
 constexpr u32 kWsCounterBytes = 256;
 // the counters are distinct u32 slots inside the 256-byte header
 constexpr u32 kWsOffsets[] = {kWsBmCounter, kWsSet1BigNext, kWsSet1SegCount, kWsSet1WholeCount, kWsBigCount,
                               kWsHugeCount, kWsSet0BigNext, kWsSet0SegCount, kWsSet0ExecNext, kWsSet0WholeCount,
-                              kWsSet1ExecNext};
+                              kWsSet1ExecNext, kWsChunkCount, kWsChunkSpecNext, kWsChunkFixNext,
+                              kWsChunkCheckNext, kWsChunkFinalNext};
 constexpr bool ws_offsets_ok() {
   for (u32 i = 0; i < sizeof(kWsOffsets) / sizeof(kWsOffsets[0]); ++i) {
     if (kWsOffsets[i] % 4 || kWsOffsets[i] + 4 > kWsCounterBytes) return false;
@@ -2135,10 +2611,15 @@ constexpr bool ws_offsets_ok() {
 }
 static_assert(ws_offsets_ok(), "workspace counters overlap or leave the header");
 constexpr u64 kListBases = 11;  // u32 arrays of n entries before the bitmap
+// The chunked pass 1b's records live at the workspace's end: 1/64 of it
+// (>= 40 bytes per 20 KiB of input: one 32-byte record per 32 KiB chunk plus
+// two words per huge message).
+constexpr u64 kChunkRegionDiv = 64;
 size_t decode_v4_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
   const u64 words = total_in_bytes / 32 + 4ull * n_msgs + 64;
-  return (size_t)(256 + kListBases * base_bytes + 4 * words);
+  const u64 base = 256 + kListBases * base_bytes + 4 * words;
+  return (size_t)(base + base / (kChunkRegionDiv - 1) + 512);
 }
 
 // Per-device side stream and fork/join events for launch_decode_v4 (created
@@ -2246,7 +2727,10 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   u64* seg_list2 = reinterpret_cast<u64*>(w + 256 + 8 * base_bytes);
   u32* whole_list2 = reinterpret_cast<u32*>(w + 256 + 10 * base_bytes);
   u32* bitmap = reinterpret_cast<u32*>(w + 256 + kListBases * base_bytes);
-  u64 cap_words = (ws_bytes - 256 - kListBases * base_bytes) / 4;
+  // chunk records (chunked pass 1b) at the end, the bitmap before them
+  const u64 chunk_bytes = (ws_bytes / kChunkRegionDiv) & ~255ull;
+  u8* const chunk_region = w + (ws_bytes - chunk_bytes);
+  u64 cap_words = (ws_bytes - chunk_bytes - 256 - kListBases * base_bytes) / 4;
   if (cap_words >= kSingleLiteral) cap_words = kSingleLiteral - 1;  // bases < 2^31 words
   // zero the counters and the bitmap (pass 1 writes only groups holding
   // tags) with one fill from the counters to the end of the bitmap: the
@@ -2375,6 +2859,46 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
         fork_big_blocks, big_threshold, 0u, keep_hist);
     return hipGetLastError();
   };
+  // The huge messages' pass 1b, chunked (chunk_*_kernel): when the record
+  // region holds a batch of this workspace's size (FSG_CHUNKED_HUGE=0: one
+  // wave per message as before).
+  const bool kChunked = [] {  // (read per call: the tests run both forms)
+    const char* e = getenv("FSG_CHUNKED_HUGE");
+    return e && e[0] == '1';
+  }();
+  const u64 max_huge = chunk_bytes / 320;
+  const u64 max_recs = max_huge ? (chunk_bytes - 8 * max_huge) / sizeof(ChunkRec) : 0;
+  u32* const first_rec = reinterpret_cast<u32*>(chunk_region);
+  u32* const mstat = first_rec + max_huge;
+  ChunkRec* const recs = reinterpret_cast<ChunkRec*>(chunk_region + 8 * max_huge);
+  const bool chunked = kChunked && max_huge >= est_total_in / kHugeIndexBytes + 1 &&
+                       max_recs >= est_total_in / kChunkBytes + est_total_in / kHugeIndexBytes + 2;
+  auto launch_big_chunked = [&](hipStream_t st, const BigSet& b) -> hipError_t {
+    u32* const cctr = reinterpret_cast<u32*>(w + kWsChunkCount);
+    const u32 lb = (u32)((max_huge + 255) / 256);
+    chunk_list_kernel<<<lb ? lb : 1u, 256, 0, st>>>(in, in_off, in_len, big_count, big_list, n_msgs, flags, cctr,
+                                                     recs, first_rec, (u32)max_recs);
+    const u32 wb = (u32)(max_recs / 4 + 1 < 1024 ? max_recs / 4 + 1 : 1024);
+    chunk_spec_kernel<<<wb, 256, 0, st>>>(in, in_off, in_len, flags, bm_base, bitmap, cctr, recs,
+                                          reinterpret_cast<u32*>(w + kWsChunkSpecNext), (u32)max_recs);
+    const u32 hb = (u32)(max_huge / 4 + 1 < 256 ? max_huge / 4 + 1 : 256);
+    chunk_fixup_kernel<<<hb, 256, 0, st>>>(in, in_off, in_len, out_len, bm_base, bitmap, big_count, recs, first_rec,
+                                           mstat, reinterpret_cast<u32*>(w + kWsChunkFixNext));
+    chunk_check_kernel<<<wb, 256, 0, st>>>(in, in_off, in_len, out_len, bm_base, bitmap, cctr, recs, out, out_off,
+                                           reinterpret_cast<u32*>(w + kWsChunkCheckNext), (u32)max_recs);
+    chunk_final_kernel<<<hb, 256, 0, st>>>(in, in_off, in_len, flags, bm_base, bitmap, out, out_off, big_list,
+                                           out_len, status, big_count, recs, first_rec, mstat, n_msgs, b.seg_list,
+                                           b.seg_count, b.whole_list, b.whole_count,
+                                           reinterpret_cast<u32*>(w + kWsChunkFinalNext));
+    hipError_t e2 = hipGetLastError();
+    if (e2 != hipSuccess) return e2;
+    const u32 fork_big_blocks = small_blocks < kBigBlocksFork ? small_blocks : kBigBlocksFork;
+    ek<<<fork_big_blocks, kWavesPerBlock * 64, 0, st>>>(
+        in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
+        reinterpret_cast<const u32*>(b.seg_list), b.seg_count, b.whole_list, b.whole_count, b.exec_next,
+        fork_big_blocks, big_threshold, 0u, keep_hist);
+    return hipGetLastError();
+  };
   auto launch_small = [&](hipStream_t st) -> hipError_t {
     // one wave per message; large ones are skipped (big_blocks = 0: no block
     // takes the large-message role)
@@ -2408,7 +2932,8 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     const bool split = kSplitHuge && side->stream2;
     if (split) {
       if ((e = hipStreamWaitEvent(side->stream2, side->fork, 0)) != hipSuccess) return e;
-      if ((e = launch_big(side->stream2, set1, 1u)) != hipSuccess) return e;
+      if ((e = chunked ? launch_big_chunked(side->stream2, set1) : launch_big(side->stream2, set1, 1u)) != hipSuccess)
+        return e;
       if ((e = hipEventRecord(side->join2, side->stream2)) != hipSuccess) return e;
     }
     if ((e = launch_big(side->stream, set0, split ? 2u : 0u)) != hipSuccess) return e;
