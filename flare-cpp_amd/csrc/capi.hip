@@ -45,6 +45,10 @@ hipError_t launch_lz4_encode(const u8* in, const u64* in_off, const u32* in_len,
 hipError_t launch_lz4_decode(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u8* out,
                              const u64* out_off, const u32* out_cap, u32* out_len, i32* status,
                              hipStream_t stream);
+size_t lz4_decode_workspace_bytes(u32 n_msgs, u64 total_in_bytes);
+hipError_t launch_lz4_decode2(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u8* out,
+                              const u64* out_off, const u32* out_cap, u32* out_len, i32* status, void* ws,
+                              size_t ws_bytes, hipStream_t stream);
 }  // namespace fsg
 
 namespace {
@@ -298,6 +302,25 @@ int fsg_lz4_decompress_batch(const uint8_t* d_in, const uint64_t* d_in_off, cons
   return record(fsg::launch_lz4_decode(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
                                        d_status, (hipStream_t)stream),
                 "fsg_lz4_decompress_batch");
+}
+
+size_t fsg_lz4_decompress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_bytes) {
+  return fsg::lz4_decode_workspace_bytes(n_msgs, total_in_bytes);
+}
+
+int fsg_lz4_decompress_batch_ws(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                                uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off,
+                                const uint32_t* d_out_cap, uint32_t* d_out_len, int32_t* d_status,
+                                void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_cap || !d_out_len || !d_status))
+    return FSG_ERR_INVALID_ARG;
+  // no usable workspace: the one-pass lane kernel (same results)
+  if (!d_workspace || workspace_bytes < fsg::lz4_decode_workspace_bytes(n_msgs, 0))
+    return fsg_lz4_decompress_batch(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                    d_status, stream);
+  return record(fsg::launch_lz4_decode2(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                        d_status, d_workspace, workspace_bytes, (hipStream_t)stream),
+                "fsg_lz4_decompress_batch_ws");
 }
 
 }  // extern "C"

@@ -254,9 +254,12 @@ __global__ __launch_bounds__(64) void lz4_decode_kernel(const u8* __restrict__ i
                                                       const u32* __restrict__ in_len, u32 n_msgs, u8* out,
                                                       const u64* __restrict__ out_off,
                                                       const u32* __restrict__ out_cap, u32* __restrict__ out_len,
-                                                      i32* __restrict__ status) {
+                                                      i32* __restrict__ status, bool fallback_only) {
   const u32 m = blockIdx.x * 64 + threadIdx.x;
   if (m >= n_msgs) return;
+  // (fallback_only: the messages lz4_decode2.hip's index pass could not
+  // index, status kNeedFallback)
+  if (fallback_only && status[m] != kNeedFallback) return;
   const u8* ib = in + in_off[m];
   const u32 n = in_len[m];
   // header: the strict varint32 form of the oracle (lz4o_header)
@@ -303,7 +306,16 @@ hipError_t launch_lz4_decode(const u8* in, const u64* in_off, const u32* in_len,
                              hipStream_t stream) {
   if (n_msgs == 0) return hipSuccess;
   lz4_decode_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off, out_cap,
-                                                           out_len, status);
+                                                           out_len, status, false);
+  return hipGetLastError();
+}
+
+hipError_t launch_lz4_decode_fallback(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u8* out,
+                                      const u64* out_off, const u32* out_cap, u32* out_len, i32* status,
+                                      hipStream_t stream) {
+  if (n_msgs == 0) return hipSuccess;
+  lz4_decode_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off, out_cap,
+                                                           out_len, status, true);
   return hipGetLastError();
 }
 

@@ -1,0 +1,729 @@
+// lz4_decode2.hip -- two-pass LZ4 block decode for gfx950 (SURVEY.md section
+// 8(f) row 4: COMPRESS_TYPE_LZ4, /root/reference/flare/rpc/options.proto:74),
+// on the machinery of the Snappy decoder (snappy_decode_v4.hip): a
+// lane-per-message index pass that validates every block and marks its
+// sequence boundaries in a bitmap, then a wave-per-message execution pass.
+//
+// Body = varint32 uncompressed length + one LZ4 block (lz4.hip).  A block is a
+// chain of sequences: token (literal-length nibble, match-length nibble),
+// literal-length extension bytes, the literals, a 2-byte offset, match-length
+// extension bytes; the last sequence stops after its literals.  Rules:
+// oracle/lz4_oracle.c lz4o_decompress_block (pinned to liblz4 1.9.3 by
+// tests/test_lz4.py).
+//
+//   pass 1, lz4_index_kernel (one LANE per message): the oracle's walk without
+//     touching output -- every check of lz4o_decompress_block, so the message's
+//     final status comes from here -- and a bitmap over the block bytes with
+//     TWO bits per sequence: its token and its offset field.  Tokens and
+//     offsets alternate, so bit 2i is token i and bit 2i+1 its offset.  Input
+//     through a per-lane LDS ring of 16-byte chunks (loads one iteration ahead
+//     of the parse), bits through a per-lane LDS ring of 128-byte groups.
+//
+//   pass 2, lz4_exec_kernel (one WAVE per message): takes up to 64 sequences
+//     per group, one per lane.  From the three positions T (token), O (offset
+//     field) and T' (next token) a lane needs only the token byte and the two
+//     offset bytes, both prefetched one group ahead:
+//       literal length  D = O - T - 1 (token + extension bytes + literals):
+//                       D <= 14: lit = D; else the extension is 255.. b with
+//                       D + 240 = 256 * n_ext + b, so lit = D - ((D + 240) >> 8)
+//       match length    E = T' - O - 2 extension bytes: E = 0: (token & 15) + 4,
+//                       E = 1: 19 + the byte at O + 2, E >= 2: long (a whole-wave
+//                       sequence, which reads the byte at T' - 1)
+//     The lane's output (literal, then match) gets its position from a prefix
+//     sum; literals and far match chunks are written in round A, near match
+//     chunks in rounds B in dependency order, in an LDS output window flushed
+//     to the slot (as the Snappy pass 2).  A sequence with more than 64
+//     literal or match bytes runs alone, by the whole wave, straight to the
+//     slot.
+//
+// Messages whose bitmap does not fit the workspace get kNeedFallback and are
+// decoded by lz4.hip's lane-per-message kernel.
+#include "wave_util.h"
+
+namespace fsg {
+
+hipError_t launch_lz4_decode_fallback(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u8* out,
+                                      const u64* out_off, const u32* out_cap, u32* out_len, i32* status,
+                                      hipStream_t stream);
+
+namespace {
+
+// ---- pass 1 geometry
+constexpr u32 kL4RingChunks = 16;  // per-lane input ring: 16 chunks of 16 bytes
+constexpr u32 kL4RingDwords = 4 * kL4RingChunks;
+constexpr u32 kL4Ahead = 6;        // chunks loaded per iteration
+constexpr int kL4Steps = 24;       // half-steps (token or offset field) per iteration
+constexpr u32 kL4BitGroups = 4;    // per-lane ring of 128-byte bit groups (4 words each)
+constexpr u32 kL4BitWords = 4 * kL4BitGroups;
+constexpr i32 kL4Parsing = -1;
+
+// ---- pass 2 geometry
+constexpr u32 kL4Waves = 4;                   // waves per block
+constexpr u32 kL4Ring = 512;                  // bitmap positions per wave
+constexpr u32 kL4FillWords = kL4Ring / 32;    // <= 512 bits: <= 342 positions (two per three bytes)
+constexpr u32 kL4Window = 3072;               // LDS output window per wave
+constexpr u32 kL4Keep = 1024;                 // history kept when it slides
+constexpr u32 kL4GroupBytes = 1024;           // output bytes per group
+constexpr u32 kL4Long = 64;                   // longer literal or match: whole-wave sequence
+constexpr u32 kL4StageMax = (kL4Window + 32) / 2 - 16;  // period staged in LDS (long overlapping match)
+static_assert(kL4Keep + kL4GroupBytes + 48 <= kL4Window, "a group fits the window after a slide");
+
+// Far chunks: earlier output of this wave, read through the slot's buffer
+// with an sc1 load (served by L2; the CU's L1 may hold a line filled before
+// the bytes were stored -- see snappy_decode_v4.hip, far_load).
+__device__ __forceinline__ u32x4 far16(__amdgpu_buffer_rsrc_t r, u32 off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+}
+
+// ===========================================================================
+// Pass 1: validate + index, one lane per message.
+__global__ __launch_bounds__(64) void lz4_index_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u32 n_msgs,
+    const u32* __restrict__ out_cap, u32* __restrict__ out_len, i32* __restrict__ status_out,
+    u32* __restrict__ bm_counter, u32* __restrict__ bm_base_out, u32* __restrict__ hdr_out,
+    u32* __restrict__ bitmap, u64 bm_capacity_words) {
+  // [dword][lane]; dword kL4RingDwords repeats dword 0 (a 4-byte read at the
+  // ring's last dword wraps)
+  __shared__ u32 ring[(kL4RingDwords + 1) * kWave];
+  __shared__ u32 bmr[kL4BitWords * kWave];
+  const u32 lane = threadIdx.x;
+  const u32 m = blockIdx.x * kWave + lane;
+  const bool valid = m < n_msgs;
+  const u8* ib = valid ? in + in_off[m] : in;
+  const u32 n_in = valid ? in_len[m] : 0u;
+
+  // header (lz4o_header: strict varint32) and slot (lz4o_decompress)
+  i32 st = kOk;
+  u32 ulen = 0, h = 0;
+  if (valid) {
+    h = (u32)parse_varint_header(ib, n_in, true, &ulen);
+    if (h == 0) {
+      st = kBadHeader;
+      out_len[m] = 0;
+    } else {
+      out_len[m] = ulen;
+      st = ulen > out_cap[m] ? kSlotTooSmall : kL4Parsing;
+    }
+  }
+  const u8* bb = ib + h;
+  const u32 n = st < 0 ? n_in - h : 0u;  // block bytes
+
+  // bitmap: round_up(ceil(n / 32), 4) words, one bump allocation per wave
+  const u32 words = st < 0 ? (((n + 31) >> 5) + 3) & ~3u : 0u;
+  const u32 incl = wave_incl_scan(words);
+  const u32 total = readlane(incl, 63);
+  u32 base0 = 0;
+  if (lane == 0 && total) base0 = atomicAdd(bm_counter, total);
+  base0 = readlane(base0, 0);
+  const u32 bmb = base0 + incl - words;
+  if (st < 0 && (u64)bmb + words > bm_capacity_words) st = kNeedFallback;
+  if (valid) {
+    bm_base_out[m] = bmb;
+    hdr_out[m] = h;
+  }
+  u32* bm = bitmap + bmb;
+
+  const u32 bal = (u32)(reinterpret_cast<uintptr_t>(bb) & 15);
+  const u8* abase = bb - bal;
+  const u32 last_chunk = n ? (bal + n - 1) >> 4 : 0u;
+  auto chunk = [&](u32 k) -> u32x4 {  // (k clamped to the block's chunks)
+    return *reinterpret_cast<const u32x4*>(abase + 16 * (k <= last_chunk ? k : last_chunk));
+  };
+  auto ring_write = [&](u32 k, u32x4 v) {
+    const u32 d = (k & (kL4RingChunks - 1)) * 4;
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i) ring[(d + i) * kWave + lane] = v[i];
+    if (d == 0) ring[kL4RingDwords * kWave + lane] = v[0];
+  };
+  // 4 bytes at block offset p, from the ring
+  auto rd4 = [&](u32 p) -> u32 {
+    const u32 P = p + bal;
+    const u32 dw = (P >> 2) & (kL4RingDwords - 1);
+    return alignbyte(ring[(dw + 1) * kWave + lane], ring[dw * kWave + lane], P & 3);
+  };
+
+  u32 wend = 0, iend = 0;  // chunks landed in the ring end at wend; loads issued end at iend
+  if (st < 0 && n) {
+    u32x4 c0[4];
+#pragma unroll
+    for (u32 c = 0; c < 4; ++c) c0[c] = chunk(c);
+#pragma unroll
+    for (u32 c = 0; c < 4; ++c)
+      if (c <= last_chunk) ring_write(c, c0[c]);
+    wend = iend = last_chunk + 1 < 4 ? last_chunk + 1 : 4u;
+  }
+#pragma unroll
+  for (u32 q = 0; q < kL4BitWords; ++q) bmr[q * kWave + lane] = 0;
+  u32 fg = 0;  // lowest bit group not yet stored
+  const u32 ngroups = words >> 2;
+
+  // walk state: pos = the next token (half 0) or offset field (half 1)
+  u32 pos = 0, op = 0, half = 0, nib = 0;
+  bool stall = false;  // a 255 extension byte: finished from global memory below
+  u32x4 g[kL4Ahead];
+#pragma unroll
+  for (u32 c = 0; c < kL4Ahead; ++c) g[c] = u32x4{0, 0, 0, 0};
+  u32 gk = 0, gn = 0;
+  __builtin_amdgcn_s_waitcnt(0);
+
+  // the rest of a token step once its literal length is known (shared with
+  // the stalled lanes' path): the checks of lz4o_decompress_block :179-184
+  auto token_tail = [&](u32 tokpos, u32 lit, u32 ipl, u32 tok) {
+    if (lit > n - ipl || lit > ulen - op) {
+      st = kCorrupt;
+      return;
+    }
+    atomicOr(&bmr[((tokpos >> 5) & (kL4BitWords - 1)) * kWave + lane], 1u << (tokpos & 31));
+    if ((u64)op + lit + 12 > ulen || (u64)ipl + lit + 8 > n) {  // the last sequence
+      st = (ipl + lit == n && op + lit == ulen) ? kOk : kCorrupt;
+      return;
+    }
+    op += lit;
+    nib = tok & 15;
+    pos = ipl + lit;
+    half = 1;
+  };
+
+  while (__any(st < 0)) {
+    // a half-step at pos reads 4 ring bytes: pos + bal + 4 <= 16 * wend, or
+    // anywhere once the ring reached the block's last chunk (bytes past the
+    // block are never used: every used byte is checked against n)
+    u32 lim = 0;
+    if (st < 0) lim = wend > last_chunk ? 0xffffffffu : (16 * wend >= bal + 4 ? 16 * wend - bal - 4 : 0u);
+#pragma unroll
+    for (int j = 0; j < kL4Steps; ++j) {
+      const bool look = st < 0 && !stall && (pos <= lim || (half == 0 && pos >= n));
+      const u32 w = rd4(pos);
+      if (look) {
+        if (half == 0) {
+          // token (:168-178)
+          const u32 tok = w & 0xffu, l0 = tok >> 4, b1 = (w >> 8) & 0xffu;
+          const bool lx = l0 == 15;
+          if (pos >= n || (lx && pos + 1 >= n)) {
+            st = kCorrupt;
+          } else if (lx && b1 == 255) {
+            stall = true;
+          } else {
+            token_tail(pos, l0 + (lx ? b1 : 0u), pos + 1 + (lx ? 1u : 0u), tok);
+          }
+        } else {
+          // offset field and match length (:188-202); pos + 8 <= n here
+          const u32 off = w & 0xffffu, b2 = (w >> 16) & 0xffu;
+          const bool mx = nib == 15;
+          const u32 ml = nib + 4 + (mx ? b2 : 0u);
+          if (off == 0 || off > op) {
+            st = kCorrupt;
+          } else if (mx && b2 == 255) {
+            stall = true;
+          } else if ((u64)ml + 5 > ulen - op) {
+            st = kCorrupt;
+          } else {
+            atomicOr(&bmr[((pos >> 5) & (kL4BitWords - 1)) * kWave + lane], 1u << (pos & 31));
+            op += ml;
+            pos += 2 + (mx ? 1u : 0u);
+            half = 0;
+          }
+        }
+      }
+    }
+    // ---------- stalled lanes: extension runs of 255s, from global memory
+    if (stall && st < 0) {
+      stall = false;
+      if (half == 0) {
+        u32 p = pos + 2, lit = 15 + 255, b;
+        bool bad = false;
+        do {
+          if (p >= n) {
+            bad = true;
+            break;
+          }
+          b = bb[p++];
+          lit += b;
+        } while (b == 255 && lit <= n);  // (lit > n fails the next check either way)
+        if (bad) st = kCorrupt;
+        else token_tail(pos, lit, p, (u32)bb[pos]);
+      } else {
+        u32 p = pos + 3, ml = 15 + 4 + 255, b;
+        bool bad = false;
+        do {
+          if (p >= n) {
+            bad = true;
+            break;
+          }
+          b = bb[p++];
+          ml += b;
+        } while (b == 255 && ml <= ulen);
+        if (bad || (u64)ml + 5 > ulen - op) {
+          st = kCorrupt;
+        } else {
+          atomicOr(&bmr[((pos >> 5) & (kL4BitWords - 1)) * kWave + lane], 1u << (pos & 31));
+          op += ml;
+          pos = p;
+          half = 0;
+        }
+      }
+    }
+
+    // ---------- store the bit groups the walk has left (every group of an
+    // OK message is stored, zero groups included: the bitmap is not zeroed)
+    if (st < 0 || st == kOk) {
+      const u32 cur = st < 0 ? pos >> 7 : ngroups;
+#pragma unroll
+      for (u32 k = 0; k < kL4BitGroups; ++k) {
+        const u32 gi = fg + k;
+        if (gi < cur) {
+          const u32 sl = (gi & (kL4BitGroups - 1)) * 4;
+          u32x4 v;
+#pragma unroll
+          for (u32 q = 0; q < 4; ++q) v[q] = bmr[(sl + q) * kWave + lane];
+          *reinterpret_cast<u32x4*>(bm + 4 * gi) = v;
+#pragma unroll
+          for (u32 q = 0; q < 4; ++q) bmr[(sl + q) * kWave + lane] = 0;
+        }
+      }
+      for (u32 gi = fg + kL4BitGroups; gi < cur; ++gi) *reinterpret_cast<u32x4*>(bm + 4 * gi) = u32x4{0, 0, 0, 0};
+      fg = cur > fg ? cur : fg;
+    }
+
+    // ---------- land last iteration's chunks, load the next ones
+#pragma unroll
+    for (u32 c = 0; c < kL4Ahead; ++c)
+      if (c < gn) ring_write(gk + c, g[c]);
+    wend = gn ? gk + gn : wend;
+    gn = 0;
+    if (st < 0) {
+      const u32 pc = (pos + bal) >> 4;
+      const u32 base = pc >= iend ? pc : iend;  // a long literal jumped past the ring: restart there
+      if (pc >= iend) wend = pc;                // (nothing at or above pc is landed)
+#pragma unroll
+      for (u32 c = 0; c < kL4Ahead; ++c) {
+        const u32 k = base + c;
+        gn += (k <= last_chunk && k <= pc + (kL4RingChunks - 1)) ? 1u : 0u;
+        g[c] = chunk(k);
+      }
+      gk = base;
+      iend = base + gn > iend ? base + gn : iend;
+    }
+  }
+  if (valid) status_out[m] = st;
+}
+
+// ===========================================================================
+// Pass 2: execute, one wave per message.
+__device__ __forceinline__ void lz4_exec_message(
+    u32 m, const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u8* out,
+    const u64* __restrict__ out_off, const u32* __restrict__ out_len, const u32* __restrict__ bm_base,
+    const u32* __restrict__ hdr, const u32* __restrict__ bitmap, u32* ring, u8* sb, const u32x4* sel_tab,
+    const u32x4* mtab, u32 lane) {
+  const u32 h = hdr[m];
+  const u32 n = in_len[m] - h;
+  const u32 expected = out_len[m];
+  const u32* bm = bitmap + bm_base[m];
+  const u8* bb = in + in_off[m] + h;
+  u8* ob = out + out_off[m];
+  const u32 bbal = (u32)(reinterpret_cast<uintptr_t>(bb) & 15);
+  const u32 obal = (u32)(reinterpret_cast<uintptr_t>(ob) & 15);
+  const __amdgpu_buffer_rsrc_t irsrc = msg_rsrc(bb - bbal, bbal + n);
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc(ob - obal, (short)0, (int)(expected + obal), 0x00020000);
+  const u32 nwords = (n + 31) >> 5;
+  constexpr u32 M = kL4Ring - 1;
+
+  u32 head = 0, tail = 0, scan = 0, op = 0;
+  int sbase = -(int)obal;  // output position of sb[0] (window blocks = the slot's 16-byte blocks)
+  u32 flushed = 0;         // output [0, flushed) is in the slot
+  auto zero_from = [&](u32 from) {
+    const u32 i = from + 16 * lane;
+    if (i < kL4Window + 32) *reinterpret_cast<u32x4*>(sb + i) = u32x4{0, 0, 0, 0};
+  };
+  zero_from(0);
+  u32 zero_end = 1024;
+  wave_lds_fence();
+  auto fill_word = [&](u32 sc) -> u32 {
+    const u32 wi = sc + (lane >> 2);
+    return (lane < 4 * kL4FillWords && wi < nwords) ? bm[wi] : 0u;
+  };
+  u32 bmw = fill_word(scan);
+  // prefetched per lane for the group at pf_head: 20 bytes from the dword
+  // below the token, 8 from the dword below the offset field
+  u32 pf_head = 0xffffffffu, pf_tail = 0;  // (entries at or above pf_tail were not in the ring yet)
+  u32x4 pd = u32x4{0, 0, 0, 0};
+  u32 pd4 = 0;
+  u32x2 po = u32x2{0, 0};
+  auto prefetch = [&](u32 t, u32 o) {
+    const u32 a = (t + bbal) & ~3u;
+    pd = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
+    pd4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
+    po = __builtin_amdgcn_raw_buffer_load_b64(irsrc, (o + bbal) & ~3u, 0, 0);
+  };
+  auto flush_to = [&](u32 fe) {
+    if (fe <= flushed) return;
+    const int b0 = (int)(((flushed + obal) & ~15u)) - (int)obal;
+    for (int blk = b0 + 16 * (int)lane; blk < (int)fe; blk += 1024) {
+      const u32 lo = blk < (int)flushed ? flushed : (u32)blk;
+      const u32 hi = blk + 16 < (int)fe ? (u32)(blk + 16) : fe;
+      if (hi - lo == 16) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(sb + (blk - sbase));
+        __builtin_memcpy(ob + blk, &v, 16);
+      } else {
+        store_exact(ob + lo, lds_read16(sb + ((int)lo - sbase)), hi - lo);
+      }
+    }
+    flushed = fe;
+  };
+
+  for (;;) {
+    // ---------- refill the position ring (a group needs 2 * 64 + 1 entries)
+    if (tail - head < 2 * 64 + 2 && scan < nwords) {
+      u32 bits = (bmw >> (8 * (lane & 3))) & 0xffu;
+      const u32 bitbase = (scan + (lane >> 2)) * 32 + 8 * (lane & 3);
+      const u32 cnt = __builtin_popcount(bits);
+      const u32 inc = dpp_incl_scan(cnt);
+      u32 slot = tail + inc - cnt;
+      while (bits) {
+        ring[slot & M] = bitbase + __builtin_ctz(bits);
+        ++slot;
+        bits &= bits - 1;
+      }
+      tail += readlane(inc, 63);
+      scan += kL4FillWords;
+      bmw = fill_word(scan);
+      wave_lds_fence();
+      continue;
+    }
+    const u32 avail = tail - head;
+    if (avail == 0 || op >= expected) break;
+    const bool done = scan >= nwords;
+    // done: the 2k - 1 entries left are k sequences, the last without offset
+    const u32 kseq = done ? ((avail + 1) >> 1 < 64 ? (avail + 1) >> 1 : 64u) : ((avail - 1) >> 1 < 64 ? (avail - 1) >> 1 : 64u);
+    const bool valid = lane < kseq;
+    const bool is_last = done && 2 * lane + 1 >= avail;
+    const u32 T = ring[(head + 2 * lane) & M];
+    const u32 O = is_last ? n : ring[(head + 2 * lane + 1) & M];
+    const u32 Tn = ring[(head + 2 * lane + 2) & M];
+    if (pf_head != head || pf_tail < head + 2 * kseq) prefetch(T, O);
+
+    // ---------- decode one sequence per lane (checked by pass 1)
+    const u32 s = (T + bbal) & 3u;
+    const u32 tok = alignbyte(pd[1], pd[0], s) & 0xffu;
+    // bytes T+1 .. T+16 (a short literal's bytes)
+    const bool q3 = s == 3;
+    const u32 w0 = q3 ? pd[1] : pd[0], w1 = q3 ? pd[2] : pd[1], w2 = q3 ? pd[3] : pd[2];
+    const u32 w3 = q3 ? pd4 : pd[3];
+    const u32 b = (s + 1) & 3u;
+    const u32x4 xr = u32x4{alignbyte(w1, w0, b), alignbyte(w2, w1, b), alignbyte(w3, w2, b), alignbyte(pd4, w3, b)};
+    const u32 D = O - T - 1;
+    const u32 lit = D <= 14 ? D : D - ((D + 240) >> 8);
+    const u32 lsrc = O - lit;
+    const u32 ow = alignbyte(po[1], po[0], (O + bbal) & 3u);  // bytes O .. O+3
+    const u32 off = ow & 0xffffu;
+    const u32 E = Tn - O - 2;
+    const u32 ml = is_last ? 0u : (E == 0 ? (tok & 15) + 4 : 19 + ((ow >> 16) & 0xffu));
+    const bool lng = valid && (lit > kL4Long || ml > kL4Long || (!is_last && E >= 2));
+    const u64 bigm = __ballot(lng);
+
+    if (bigm & 1ull) {
+      // ---------- a long sequence: the whole wave, straight to the slot
+      const u32 L = readlane(lit, 0), S = readlane(lsrc, 0);
+      const bool last0 = readlane(is_last ? 1u : 0u, 0) != 0;
+      const u32 OFF = readlane(off, 0), E0 = readlane(E, 0), Tn0 = readlane(Tn, 0);
+      u32 ML = last0 ? 0u : readlane(ml, 0);
+      if (!last0 && E0 >= 2) {  // 19 + 255 (E - 1) + the last extension byte
+        const u32 P = Tn0 - 1 + bbal;
+        const u32 x = __builtin_amdgcn_raw_buffer_load_b32(irsrc, P & ~3u, 0, 0);
+        ML = 19 + 255 * (E0 - 1) + ((x >> (8 * (P & 3))) & 0xffu);
+      }
+      flush_to(op);
+      for (u32 k0 = 0; k0 < L; k0 += 4096) {  // literal: 4 KiB per step, loads first
+        Raw16 x[4];
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) x[r] = raw_load16(irsrc, S + k0 + 1024 * r + lane * 16 + bbal);
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) {
+          const u32 k = k0 + 1024 * r + lane * 16;
+          if (k < L) store_exact(ob + op + k, shifted16(x[r]), L - k < 16 ? L - k : 16u);
+        }
+      }
+      op += L;
+      if (ML) {
+        wait_all_memory();  // every byte below op is in the slot (L2)
+        const u32 d = op, src = op - OFF;
+        if (OFF >= ML) {  // no overlap: a straight copy
+          for (u32 k0 = 0; k0 < ML; k0 += 4096) {
+            u32x4 x[4];
+#pragma unroll
+            for (u32 r = 0; r < 4; ++r) x[r] = far16(orsrc, src + k0 + 1024 * r + lane * 16 + obal);
+#pragma unroll
+            for (u32 r = 0; r < 4; ++r) {
+              const u32 k = k0 + 1024 * r + lane * 16;
+              if (k < ML) store_exact(ob + d + k, x[r], ML - k < 16 ? ML - k : 16u);
+            }
+          }
+        } else if (OFF < 16) {  // period < 16: every piece is the same expanded pattern
+          const u32x4 P = expand_pattern(far16(orsrc, src + obal), OFF, sel_tab);
+          const u32 stp = pat_step(OFF);
+          for (u32 k = lane * stp; k < ML; k += 64 * stp) store_exact(ob + d + k, P, ML - k < stp ? ML - k : stp);
+        } else if (OFF <= kL4StageMax) {
+          // period OFF staged twice in the window (free until the restart
+          // below): chunk j reads its 16 bytes at phase 16 j mod OFF
+          for (u32 i = 16 * lane; i < OFF; i += 1024) {
+            const u32x4 x = far16(orsrc, src + i + obal);
+            const u32 c = OFF - i < 16 ? OFF - i : 16u;
+            store_exact(sb + i, x, c);
+            store_exact(sb + OFF + i, x, c);
+          }
+          wave_lds_fence();
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the staged bytes are in LDS
+          u32 ph = (16 * lane) % OFF;
+          const u32 inc = 1024 % OFF;
+          for (u32 k = 16 * lane; k < ML; k += 1024) {
+            store_exact(ob + d + k, lds_read16(sb + ph), ML - k < 16 ? ML - k : 16u);
+            ph += inc;
+            ph = ph >= OFF ? ph - OFF : ph;
+          }
+        } else {
+          // a long period: steps of at most OFF bytes, each reading only
+          // bytes the earlier steps stored
+          const u32 step = (OFF & ~15u) < 4096 ? (OFF & ~15u) : 4096u;
+          for (u32 k0 = 0; k0 < ML; k0 += step) {
+            const u32 e = k0 + step < ML ? k0 + step : ML;
+            for (u32 k = k0 + 16 * lane; k < e; k += 1024)
+              store_exact(ob + d + k, far16(orsrc, src + k + obal), e - k < 16 ? e - k : 16u);
+            wait_all_memory();
+          }
+        }
+        op += ML;
+      }
+      // restart the window one block before the block holding op; its head
+      // (the bytes [sbase, op)) comes back from the slot
+      wait_all_memory();
+      sbase = (int)((op + obal) & ~15u) - (int)obal - 16;
+      zero_from(0);
+      zero_end = 1024;
+      wave_lds_fence();
+      if (lane < 2) {
+        const int lo = sbase + 16 * (int)lane;
+        if (lo >= 0 && (u32)lo < op) {
+          const u32 c = op - (u32)lo < 16 ? op - (u32)lo : 16u;
+          store_exact(sb + 16 * lane, far16(orsrc, (u32)lo + obal), c);
+        }
+      }
+      wave_lds_fence();
+      flushed = op;
+      head += last0 ? 1u : 2u;
+      pf_head = 0xffffffffu;
+      // the sequence's bytes hold no other positions: resume the bitmap scan
+      // at the next token's word
+      if (head == tail && !last0) {
+        const u32 nw = Tn0 >> 5;
+        if (nw > scan) {
+          scan = nw;
+          bmw = fill_word(scan);
+        }
+      }
+      continue;
+    }
+    const u32 take = bigm ? (u32)__builtin_ctzll(bigm) : kseq;
+    const bool v = lane < take;
+
+    // ---------- output positions: <= kL4GroupBytes per group
+    const u32 len = v ? lit + ml : 0u;
+    const u32 incl = dpp_incl_scan(len);
+    const u32 t_op = op + incl - len;
+    const bool fits = v && incl <= kL4GroupBytes;
+    const u32 k_seq = (u32)__builtin_popcountll(__ballot(fits));
+    const u32 tot = readlane(incl, k_seq - 1);
+    const bool group_last = readlane(is_last ? 1u : 0u, k_seq - 1) != 0;
+
+    // ---------- slide the window if this group would overrun it
+    if (op + tot - sbase > kL4Window) {
+      const int nsb = (int)(((op - kL4Keep + obal) & ~15u)) - (int)obal;
+      // far chunks may read up to 15 bytes at and above the new base
+      if ((int)flushed < nsb + 16) flush_to((u32)((int)((op + obal) & ~15u) - (int)obal));
+      wait_all_memory();
+      const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
+      for (u32 k = 0; k < keep; k += 1024) {
+        const u32 i = k + 16 * lane;
+        u32x4 x = u32x4{0, 0, 0, 0};
+        if (i < keep) x = *reinterpret_cast<const u32x4*>(sb + shift + i);
+        wave_lds_fence();
+        if (i < keep) *reinterpret_cast<u32x4*>(sb + i) = x;
+        wave_lds_fence();
+      }
+      sbase = nsb;
+      zero_end = (keep + 15) & ~15u;
+    }
+    // ---------- prefetch the next group
+    {
+      const u32 nh = head + 2 * k_seq;
+      const u32 nT = ring[(nh + 2 * lane) & M];
+      const u32 nO = ring[(nh + 2 * lane + 1) & M];
+      prefetch(nT, nO);
+      pf_head = nh;
+      pf_tail = tail;
+    }
+    while (op + tot + 20 - sbase > zero_end) {
+      zero_from(zero_end);
+      zero_end += 1024;
+    }
+    wave_lds_fence();
+
+    // ---------- round A: literals (registers for <= 14 bytes, else the
+    // input) and the match's leading chunks whose source starts below the
+    // window base (the slot)
+    const u32 mo = t_op + lit - off;  // match source
+    const bool pat = off < 16 && off < ml;
+    const u32 nch = (ml + 15) >> 4;
+    const u32 below = (u32)(sbase - (int)mo);
+    const u32 kfar = (int)below > 0 ? ((below - 1) >> 4) + 1 : 0u;
+    const u32 kc = (!fits || is_last || pat) ? 0u : (kfar < nch ? kfar : nch);
+    const u32 nlc = fits ? (lit + 15) >> 4 : 0u;
+    const bool reg0 = lit <= 14;
+    const u32 wa = (u32)((int)t_op - sbase);
+    const u32 wm = wa + lit;
+    // items: literal chunks [0, nlc), then far chunks [0, kc); two per pass
+    const u32 nit = nlc + kc;
+    // the previous groups' completed blocks, 1 KiB at a time
+    auto flush_group = [&]() {
+      const int fe = (int)((op + obal) & ~15u) - (int)obal;
+      if (fe >= (int)flushed + 1024) flush_to((u32)fe);
+    };
+    if (!__ballot(nit > 0)) flush_group();
+    for (u32 i0 = 0; __ballot(i0 < nit); i0 += 2) {
+      u32x4 x0 = u32x4{0, 0, 0, 0}, x1 = u32x4{0, 0, 0, 0};
+      u32 y0 = 0, y1 = 0;
+      bool l0 = false, l1 = false;  // item is a literal chunk
+      auto issue = [&](u32 it, u32x4& x, u32& y, bool& isl) {
+        if (it >= nit) return;
+        if (it < nlc) {
+          isl = true;
+          if (it == 0 && reg0) {
+            x = xr;
+            y = 0xffffffffu;  // marker: already shifted
+          } else {
+            const u32 a = (lsrc + 16 * it + bbal) & ~3u;
+            x = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
+            y = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
+          }
+        } else {
+          x = far16(orsrc, mo + 16 * (it - nlc) + obal);
+        }
+      };
+      issue(i0, x0, y0, l0);
+      issue(i0 + 1, x1, y1, l1);
+      if (i0 == 0) flush_group();  // while the loads are in flight
+      auto land = [&](u32 it, u32x4 x, u32 y, bool isl) {
+        if (it >= nit) return;
+        if (isl) {
+          if (!(it == 0 && reg0)) {
+            const u32 sh = (lsrc + 16 * it + bbal) & 3u;
+            x = u32x4{alignbyte(x[1], x[0], sh), alignbyte(x[2], x[1], sh), alignbyte(x[3], x[2], sh),
+                      alignbyte(y, x[3], sh)};
+          }
+          const u32 r = lit - 16 * it;
+          or_store(sb, wa + 16 * it, x, r < 16 ? r : 16u, mtab);
+        } else {
+          const u32 k = it - nlc;
+          const u32 r = ml - 16 * k;
+          or_store(sb, wm + 16 * k, x, r < 16 ? r : 16u, mtab);
+        }
+      };
+      land(i0, x0, y0, l0);
+      land(i0 + 1, x1, y1, l1);
+    }
+    wave_lds_fence();
+
+    // ---------- rounds B: the near match chunks in dependency order (as the
+    // Snappy pass 2: a chunk runs once its source ends at or below the first
+    // unfinished chunk; read-modify-write merges exactly n bytes)
+    u32 rem = (fits && !is_last && kc < nch) ? ml - 16 * kc : 0u;
+    u32 cw = wm + 16 * kc;
+    u32 sw = (u32)((int)mo - sbase) + 16 * kc;
+    const u32 stp = pat ? pat_step(off) : 16u;
+    u32 nb = rem < stp ? rem : stp;
+    bool pf = pat;
+    u32 ne = rem ? (pf ? cw : sw + nb) : 0xffffffffu;
+    u64 pend = __ballot(rem > 0);
+    while (pend) {
+      const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
+      if (ne <= W) {
+        u32x4 x = lds_read16(sb + sw);
+        if (pf) x = expand_pattern(x, off, sel_tab);
+        const u32x4 o = lds_read16(sb + cw);
+        const u32x4 mk = mtab[nb];
+        u32x4 y;
+        y[0] = (x[0] & mk[0]) | (o[0] & ~mk[0]);
+        y[1] = (x[1] & mk[1]) | (o[1] & ~mk[1]);
+        y[2] = (x[2] & mk[2]) | (o[2] & ~mk[2]);
+        y[3] = (x[3] & mk[3]) | (o[3] & ~mk[3]);
+        __builtin_memcpy(sb + cw, &y, 16);
+        rem -= nb;
+        cw += nb;
+        sw = pat ? cw - stp : sw + nb;
+        pf = false;
+        nb = rem < stp ? rem : stp;
+        ne = rem ? sw + nb : 0xffffffffu;
+      }
+      wave_lds_fence();
+      pend = __ballot(rem > 0);
+    }
+    op += tot;
+    head += group_last ? 2 * k_seq - 1 : 2 * k_seq;
+  }
+  flush_to(expected);
+}
+
+__global__ __launch_bounds__(kL4Waves * 64) void lz4_exec_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u32 n_msgs,
+    u8* out, const u64* __restrict__ out_off, const u32* __restrict__ out_len, const i32* __restrict__ status,
+    const u32* __restrict__ bm_base, const u32* __restrict__ hdr, const u32* __restrict__ bitmap) {
+  __shared__ __attribute__((aligned(16))) u8 wl_s[kL4Waves][4 * kL4Ring + kL4Window + 32];
+  __shared__ u32x4 sel_tab[16];
+  __shared__ u32x4 mask_tab[17];
+  if (threadIdx.x < 64) init_pattern_table(sel_tab, threadIdx.x);
+  init_mask_table(mask_tab, threadIdx.x);
+  __syncthreads();
+  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const u32 lane = threadIdx.x & 63;
+  const u32 m = blockIdx.x * kL4Waves + wv;
+  if (m >= n_msgs || status[m] != kOk || out_len[m] == 0) return;
+  lz4_exec_message(m, in, in_off, in_len, out, out_off, out_len, bm_base, hdr, bitmap,
+                   reinterpret_cast<u32*>(wl_s[wv]), wl_s[wv] + 4 * kL4Ring, sel_tab, mask_tab, lane);
+}
+
+}  // namespace
+
+// Workspace: [0, 256) counters | bm_base[n] | hdr[n] | bitmap words
+// (round_up(ceil(block / 32), 4) per message <= total / 32 + 4 n).
+constexpr u64 kL4Head = 256;
+__host__ u64 l4_list_bytes(u32 n) { return ((u64)n * 4 + 255) & ~(u64)255; }
+size_t lz4_decode_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
+  return kL4Head + 2 * l4_list_bytes(n_msgs) + 4 * (total_in_bytes / 32 + 4 * (u64)n_msgs + 4);
+}
+
+hipError_t launch_lz4_decode2(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u8* out,
+                              const u64* out_off, const u32* out_cap, u32* out_len, i32* status, void* ws,
+                              size_t ws_bytes, hipStream_t stream) {
+  if (n_msgs == 0) return hipSuccess;
+  const u64 fixed = kL4Head + 2 * l4_list_bytes(n_msgs);
+  if (ws_bytes < fixed) return hipErrorInvalidValue;
+  u8* w = static_cast<u8*>(ws);
+  u32* counter = reinterpret_cast<u32*>(w);
+  u32* bm_base = reinterpret_cast<u32*>(w + kL4Head);
+  u32* hdr = reinterpret_cast<u32*>(w + kL4Head + l4_list_bytes(n_msgs));
+  u32* bitmap = reinterpret_cast<u32*>(w + fixed);
+  const u64 cap_words = (ws_bytes - fixed) / 16 * 4;  // whole 16-byte groups
+  hipError_t e = hipMemsetAsync(counter, 0, kL4Head, stream);
+  if (e != hipSuccess) return e;
+  lz4_index_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out_cap, out_len, status,
+                                                         counter, bm_base, hdr, bitmap, cap_words);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  lz4_exec_kernel<<<(n_msgs + kL4Waves - 1) / kL4Waves, kL4Waves * 64, 0, stream>>>(
+      in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, hdr, bitmap);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_lz4_decode_fallback(in, in_off, in_len, n_msgs, out, out_off, out_cap, out_len, status, stream);
+}
+
+}  // namespace fsg

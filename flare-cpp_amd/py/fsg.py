@@ -44,6 +44,8 @@ _SIGS = {
     "fsg_lz4_compress_workspace_bytes": (_sz, [_u32]),
     "fsg_lz4_compress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "fsg_lz4_decompress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "fsg_lz4_decompress_workspace_bytes": (_sz, [_u32, _u64]),
+    "fsg_lz4_decompress_batch_ws": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
 }
 
 
@@ -150,11 +152,24 @@ class SnappyGPU:
             _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off), _ptr(d_out_len),
             _ptr(d_status), _ptr(workspace), workspace.numel(), self._stream(stream)), "fsg_lz4_compress_batch")
 
+    def lz4_decompress_workspace(self, n, total_in_bytes, device=None):
+        import torch
+        nbytes = self.lib.fsg_lz4_decompress_workspace_bytes(n, total_in_bytes)
+        return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device or f"cuda:{self.device}")
+
     def lz4_decompress(self, d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len, d_status,
-                       stream=None):
-        self._check(self.lib.fsg_lz4_decompress_batch(
+                       stream=None, workspace=None):
+        """workspace=None: the one-pass lane kernel; else the two-pass
+        decoder (fsg_lz4_decompress_batch_ws)."""
+        if workspace is None:
+            self._check(self.lib.fsg_lz4_decompress_batch(
+                _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off), _ptr(d_out_cap),
+                _ptr(d_out_len), _ptr(d_status), self._stream(stream)), "fsg_lz4_decompress_batch")
+            return
+        self._check(self.lib.fsg_lz4_decompress_batch_ws(
             _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off), _ptr(d_out_cap),
-            _ptr(d_out_len), _ptr(d_status), self._stream(stream)), "fsg_lz4_decompress_batch")
+            _ptr(d_out_len), _ptr(d_status), _ptr(workspace), workspace.numel(), self._stream(stream)),
+            "fsg_lz4_decompress_batch_ws")
 
     def uncompressed_lengths(self, d_in, d_in_off, d_in_len, n, d_ulen, lenient=True, stream=None):
         self._check(self.lib.fsg_uncompressed_lengths_batch(

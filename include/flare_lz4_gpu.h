@@ -56,6 +56,23 @@ int fsg_lz4_decompress_batch(const uint8_t *d_in, const uint64_t *d_in_off,
                              const uint32_t *d_out_cap, uint32_t *d_out_len,
                              int32_t *d_status, void *stream);
 
+/* Device workspace for fsg_lz4_decompress_batch_ws: counters, two u32 per
+ * message and the sequence bitmap (one bit per block byte). */
+size_t fsg_lz4_decompress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_bytes);
+
+/* fsg_lz4_decompress_batch (same arguments, statuses and bytes) on the
+ * two-pass decoder: a lane-per-message index pass (validation + sequence
+ * bitmap), then a wave-per-message execution pass.  Messages whose bitmap
+ * does not fit the workspace, or every message when d_workspace is NULL or
+ * smaller than fsg_lz4_decompress_workspace_bytes(n_msgs, 0), run the
+ * one-pass kernel. */
+int fsg_lz4_decompress_batch_ws(const uint8_t *d_in, const uint64_t *d_in_off,
+                                const uint32_t *d_in_len, uint32_t n_msgs,
+                                uint8_t *d_out, const uint64_t *d_out_off,
+                                const uint32_t *d_out_cap, uint32_t *d_out_len,
+                                int32_t *d_status, void *d_workspace,
+                                size_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -95,7 +95,11 @@ class GpuCodec:
         st = d_st.cpu().numpy()[:n]
         return [out[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() for i in range(n)], st
 
-    def lz4_decompress(self, bodies: list[bytes], caps: list[int]):
+    def lz4_decompress(self, bodies: list[bytes], caps: list[int], two_pass: bool = True,
+                       ws_total_in: int | None = None, ws_fill: int | None = None):
+        """two_pass: fsg_lz4_decompress_batch_ws with a workspace sized for
+        ws_total_in input bytes (default: the real size; smaller values send
+        messages to the one-pass fallback), filled with ws_fill first."""
         torch = self.torch
         b = fsg.Batch.from_list(bodies)
         n = len(b)
@@ -104,7 +108,13 @@ class GpuCodec:
         d_out = torch.full((max(tot, 1),), POISON, dtype=torch.uint8, device="cuda")
         d_ol = empty(n, torch.int32)
         d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")
-        self.codec.lz4_decompress(dev(b.data), dev(b.offsets), dev(b.lens), n, d_out, dev(oo), dev(caps), d_ol, d_st)
+        ws = None
+        if two_pass:
+            ws = self.codec.lz4_decompress_workspace(n, int(b.data.size) if ws_total_in is None else ws_total_in)
+            if ws_fill is not None:
+                ws.fill_(ws_fill)
+        self.codec.lz4_decompress(dev(b.data), dev(b.offsets), dev(b.lens), n, d_out, dev(oo), dev(caps), d_ol, d_st,
+                                  workspace=ws)
         torch.cuda.synchronize()
         out = d_out.cpu().numpy()
         ol = d_ol.cpu().numpy()[:n].view(np.uint32)

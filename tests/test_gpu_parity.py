@@ -154,23 +154,30 @@ def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, monkeypatch):
     gpu.codec.select_kernels(0, 0)
 
 
-@pytest.mark.parametrize("fork", ["0", "1"])
+@pytest.mark.parametrize("fork", ["0", "1", "1c"])
 def test_large_message_index_fuzz(gpu, oracle, fork, monkeypatch):
     """Compressed bodies over 48 KiB take the wave-per-message index pass
     (index_big_kernel): intact, bit-flipped and truncated ones, mixed with
     small ones in one batch, against the oracle's verdicts and bytes.  With
     FSG_DECODE_FORK=1 pass 1b and the large-message exec blocks run on the
     library's side stream beside the small messages' exec launch (the
-    default for batches of > 128K messages)."""
-    monkeypatch.setenv("FSG_DECODE_FORK", fork)
+    default for batches of > 128K messages).  "1c": the huge bodies (> 256 KiB
+    compressed) through the chunked pass 1b (FSG_CHUNKED_HUGE=1), corruption
+    in every chunk position included."""
+    monkeypatch.setenv("FSG_DECODE_FORK", fork[0])
+    monkeypatch.setenv("FSG_CHUNKED_HUGE", "1" if fork == "1c" else "0")
     rng = np.random.default_rng(21)
     srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (120000, 400000, 1 << 20)]
+    if fork == "1c":  # more huge bodies: 3 MiB text, text with a long random run across chunks
+        srcs.append(fsg.make_batch(fsg.KIND_TEXT, [3 << 20], first_index=77).item(0))
+        t = fsg.make_batch(fsg.KIND_TEXT, [900000], first_index=78).item(0)
+        srcs.append(t[:300000] + fsg.make_batch(fsg.KIND_RANDOM, [100000], first_index=79).item(0) + t[300000:])
     srcs.append(fsg.make_batch(fsg.KIND_RANDOM, [70000]).item(0))
     srcs.append(fsg.make_batch(fsg.KIND_TEXT, [3000]).item(0))  # small, lane path
     base = [oracle.compress(s) for s in srcs]
     assert all(len(c) > 48 * 1024 for c in base[:4])
     comps, caps = [], []
-    for i in range(160):
+    for i in range(160 if fork != "1c" else 224):
         c = bytearray(base[i % len(base)])
         mode = i // len(base) % 4
         if mode == 1:
@@ -181,10 +188,10 @@ def test_large_message_index_fuzz(gpu, oracle, fork, monkeypatch):
         elif mode == 3:  # corrupt late in the stream
             c[len(c) - 1 - int(rng.integers(min(64, len(c) - 1)))] ^= 0x5A
         comps.append(bytes(c))
-        caps.append(1 << 21)
+        caps.append(1 << 22)
     outs, ol, st = gpu.decompress(comps, caps)
     for i, (c, o, l, s) in enumerate(zip(comps, outs, ol, st)):
-        ok, ulen, ref = oracle.uncompress(c, cap=1 << 21)
+        ok, ulen, ref = oracle.uncompress(c, cap=1 << 22)
         if ok is None:
             assert s == fsg.FSG_SLOT_TOO_SMALL, i
         elif not ok:
@@ -402,14 +409,22 @@ def _copy2(length: int, offset: int) -> bytes:
     return bytes([((length - 1) << 2) | 2]) + offset.to_bytes(2, "little")
 
 
-@pytest.mark.parametrize("fork", ["0", "1"])
+def _copy4(length: int, offset: int) -> bytes:
+    """COPY_4_BYTE_OFFSET tag (len 1..64)."""
+    return bytes([((length - 1) << 2) | 3]) + offset.to_bytes(4, "little")
+
+
+@pytest.mark.parametrize("fork", ["0", "1", "1c"])
 def test_large_message_segments(gpu, oracle, fork, monkeypatch):
     """Large bodies run in pass 2 as 64 KiB output segments when no tag spans
     a segment boundary and no copy reaches below its segment (every stream the
     reference encoder writes); otherwise whole.  Raw sizes around the
     boundaries, a tail of < 4 bytes (joins the previous segment), and
-    hand-built streams that must run whole; on one stream and forked."""
-    monkeypatch.setenv("FSG_DECODE_FORK", fork)
+    hand-built streams that must run whole; on one stream and forked ("1c":
+    the huge bodies through the chunked pass 1b, huge hand-built streams that
+    must run whole included)."""
+    monkeypatch.setenv("FSG_DECODE_FORK", fork[0])
+    monkeypatch.setenv("FSG_CHUNKED_HUGE", "1" if fork == "1c" else "0")
     rng = np.random.default_rng(5)
     items = []
     for n in (65537, 131072, 131073, 131074, 131075, 131076, 196609, 300000, 1 << 20):
@@ -426,9 +441,17 @@ def test_large_message_segments(gpu, oracle, fork, monkeypatch):
                  + _copy2(64, 1000) * 10)
     comps += [oracle.compress(fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0))
               for s in (100, 5000, 20000)]
-    outs, ol, st = gpu.decompress(comps, [1 << 21] * len(comps))
+    if fork == "1c":
+        big = rng.integers(0, 256, 400000, dtype=np.uint8).tobytes()
+        # huge (> 256 KiB compressed): a copy at output 400000 reaching below its segment
+        comps.append(_varint(len(big) + 64) + _literal(big) + _copy4(64, 70000))
+        # huge, copies spanning 64 KiB boundaries after a long literal
+        comps.append(_varint(300000 + 64 * 4000) + _literal(big[:300000]) + _copy2(64, 30000) * 4000)
+        # huge text of 2 MiB and 3 MiB (segmentable)
+        comps += [oracle.compress(fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0)) for s in (2 << 20, 3 << 20)]
+    outs, ol, st = gpu.decompress(comps, [1 << 22] * len(comps))
     for i, (c, o, s) in enumerate(zip(comps, outs, st)):
-        ok, ulen, ref = oracle.uncompress(c, cap=1 << 21)
+        ok, ulen, ref = oracle.uncompress(c, cap=1 << 22)
         assert ok, i
         assert s == fsg.FSG_OK and o[:ulen] == ref, (i, s)
 

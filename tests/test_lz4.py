@@ -213,3 +213,14 @@ def test_gpu_block_codec_on_host_asan(host_check, o, tmp_path):
         if ok:
             assert out[p:p + u] == y
             p += u
+
+
+def test_synthetic_blocks_valid_under_oracle(o):
+    """tests/lz4_blocks.py (the two-pass GPU decoder's edge-case inputs):
+    every block it builds is accepted by the oracle with the expected bytes."""
+    from lz4_blocks import random_block
+    rng = np.random.default_rng(5)
+    for t in range(40):
+        body, want = random_block(rng, int(rng.choice([100, 5000, 70000])))
+        r, ulen, got = o.uncompress(body, cap=len(want))
+        assert r == 1 and ulen == len(want) and got == want, t

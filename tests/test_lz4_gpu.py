@@ -1,6 +1,8 @@
-"""GPU parity of the LZ4 path (flare-cpp_amd/csrc/lz4.hip) through the C ABI
-(include/flare_lz4_gpu.h): bodies byte-equal to the oracle and to the liblz4
-fixtures, every decode verdict and byte equal to the oracle's."""
+"""GPU parity of the LZ4 path (flare-cpp_amd/csrc/lz4.hip, lz4_decode2.hip)
+through the C ABI (include/flare_lz4_gpu.h): bodies byte-equal to the oracle
+and to the liblz4 fixtures, every decode verdict and byte equal to the
+oracle's -- for the one-pass lane decoder (fsg_lz4_decompress_batch) and the
+two-pass decoder (fsg_lz4_decompress_batch_ws)."""
 import json
 from pathlib import Path
 
@@ -39,7 +41,12 @@ def _header(n: int) -> bytes:
     return bytes(out)
 
 
-def test_lz4_compress_matches_liblz4_fixtures(gpu, o):
+@pytest.fixture(params=[False, True], ids=["one_pass", "two_pass"])
+def two(request):
+    return request.param
+
+
+def test_lz4_compress_matches_liblz4_fixtures(gpu, o, two):
     vecs = [v for v in VEC["compress"] if v["input_len"] <= 1 << 20]
     xs = [build_input(v) for v in vecs]
     bodies, st = gpu.lz4_compress(fsg.Batch.from_list(xs))
@@ -50,12 +57,12 @@ def test_lz4_compress_matches_liblz4_fixtures(gpu, o):
         blk = body[len(h):]
         assert len(blk) == v["block_len"] and "%016x" % fsg.fnv1a64(blk) == v["block_fnv"], v["name"]
         assert body == o.compress(x), v["name"]
-    outs, ol, st = gpu.lz4_decompress(bodies, [len(x) for x in xs])
+    outs, ol, st = gpu.lz4_decompress(bodies, [len(x) for x in xs], two_pass=two)
     assert (st == fsg.FSG_OK).all()
     assert all(y == x for y, x in zip(outs, xs))
 
 
-def test_lz4_randomized_against_oracle(gpu, o):
+def test_lz4_randomized_against_oracle(gpu, o, two):
     rng = np.random.default_rng(17)
     xs = []
     for t in range(600):
@@ -68,11 +75,11 @@ def test_lz4_randomized_against_oracle(gpu, o):
     assert (st == 0).all()
     for x, b in zip(xs, bodies):
         assert b == o.compress(x), len(x)
-    outs, ol, st = gpu.lz4_decompress(bodies, [len(x) for x in xs])
+    outs, ol, st = gpu.lz4_decompress(bodies, [len(x) for x in xs], two_pass=two)
     assert (st == 0).all() and all(y == x for y, x in zip(outs, xs))
 
 
-def test_lz4_decode_verdicts_against_oracle(gpu, o):
+def test_lz4_decode_verdicts_against_oracle(gpu, o, two):
     cases = VEC["decode"]
     bodies = [_header(d["ulen"]) + bytes.fromhex(d["hex"]) for d in cases]
     rng = np.random.default_rng(3)
@@ -85,7 +92,7 @@ def test_lz4_decode_verdicts_against_oracle(gpu, o):
             b = b[:int(rng.integers(1, len(b) + 1))]
         bodies.append(bytes(b))
     cap = 1 << 16
-    outs, ol, st = gpu.lz4_decompress(bodies, [cap] * len(bodies))
+    outs, ol, st = gpu.lz4_decompress(bodies, [cap] * len(bodies), two_pass=two)
     for i, (b, y, l, s) in enumerate(zip(bodies, outs, ol, st)):
         r, ulen, ref = o.uncompress(b, cap=cap)
         want = {1: fsg.FSG_OK, 0: fsg.FSG_CORRUPT, -1: fsg.FSG_BAD_HEADER, -2: fsg.FSG_SLOT_TOO_SMALL}[r]
@@ -97,10 +104,93 @@ def test_lz4_decode_verdicts_against_oracle(gpu, o):
             assert (s == fsg.FSG_OK) == d["liblz4_ok"]
 
 
-def test_lz4_empty_and_edges(gpu, o):
+def test_lz4_empty_and_edges(gpu, o, two):
     xs = [b"", b"x", b"a" * 12, b"a" * 13, bytes(65547)]
     bodies, st = gpu.lz4_compress(fsg.Batch.from_list(xs))
     assert (st == 0).all() and bodies[0] == b"\x00\x00"
-    outs, ol, st = gpu.lz4_decompress(bodies + [b"", b"\x05\x50hello"], [len(x) for x in xs] + [0, 4])
+    outs, ol, st = gpu.lz4_decompress(bodies + [b"", b"\x05\x50hello"], [len(x) for x in xs] + [0, 4],
+                                      two_pass=two)
     assert list(st) == [0] * 5 + [fsg.FSG_BAD_HEADER, fsg.FSG_SLOT_TOO_SMALL]
     assert outs[:5] == xs
+
+
+def _kinds(rng, n):
+    """Bodies of every kind the bench and the RPC path see, 0 B .. 2 MiB."""
+    out = []
+    for i in range(n):
+        k = i % 6
+        size = int(rng.choice([0, 1, 13, 200, 4096, 65536, 65547, 100000, 300000, 1 << 21]))
+        if k == 0:
+            x = fsg.make_batch(fsg.KIND_TEXT, [size], first_index=i).item(0) if size else b""
+        elif k == 1:
+            x = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        elif k == 2:
+            x = bytes(size)
+        elif k == 3:
+            x = (bytes(rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8)) * (size // 2 + 1))[:size]
+        elif k == 4:
+            x = rng.integers(0, 3, size, dtype=np.uint8).tobytes()
+        else:
+            x = fsg.make_batch(fsg.KIND_PROTO, [size], first_index=i).item(0) if size else b""
+        out.append(x)
+    return out
+
+
+def test_lz4_two_pass_kinds_against_oracle(gpu, o):
+    """Compressor output of every kind and size (long literals of random
+    bodies, long runs of zeros, short periods, text, JSON) through the
+    two-pass decoder: bytes equal to the inputs, statuses OK."""
+    rng = np.random.default_rng(31)
+    xs = _kinds(rng, 60)
+    bodies = [o.compress(x) for x in xs]
+    outs, ol, st = gpu.lz4_decompress(bodies, [len(x) for x in xs])
+    assert (st == 0).all()
+    for i, (y, x) in enumerate(zip(outs, xs)):
+        assert y == x, (i, len(x))
+
+
+def test_lz4_two_pass_synthetic_sequences(gpu, o):
+    """Blocks built sequence by sequence (tests/lz4_blocks.py): every
+    extension-byte boundary of both lengths, 255 runs, empty literals,
+    offsets 1..15 / 16..1536 / above, matches longer than their offset and
+    tens of KiB long -- the whole-wave path of the execution pass."""
+    from lz4_blocks import random_block
+    rng = np.random.default_rng(41)
+    bodies, wants = [], []
+    for t in range(120):
+        b, w = random_block(rng, int(rng.choice([50, 3000, 40000, 200000])))
+        bodies.append(b)
+        wants.append(w)
+    outs, ol, st = gpu.lz4_decompress(bodies, [len(w) for w in wants])
+    for i, (b, y, w, s) in enumerate(zip(bodies, outs, wants, st)):
+        assert s == 0 and y == w, i
+
+
+def test_lz4_two_pass_workspace_garbage_and_fallback(gpu, o):
+    """The workspace may hold anything (filled with 0xff first), and one
+    sized for less input than the batch sends the messages whose bitmap does
+    not fit to the one-pass kernel: the same bytes and statuses either way."""
+    rng = np.random.default_rng(7)
+    xs = _kinds(rng, 36)
+    bodies = [o.compress(x) for x in xs]
+    bodies[3] = bodies[3][:-1] if len(bodies[3]) > 2 else bodies[3]  # a truncated one among them
+    caps = [len(x) for x in xs]
+    ref = [o.uncompress(b, cap=c) for b, c in zip(bodies, caps)]
+    want_st = [{1: 0, 0: fsg.FSG_CORRUPT, -1: fsg.FSG_BAD_HEADER, -2: fsg.FSG_SLOT_TOO_SMALL}[r] for r, _, _ in ref]
+    for kw in ({"ws_fill": 0xFF}, {"ws_total_in": sum(map(len, bodies)) // 3, "ws_fill": 0x5A}):
+        outs, ol, st = gpu.lz4_decompress(bodies, caps, **kw)
+        assert list(st) == want_st, kw
+        for (r, _, y0), y in zip(ref, outs):
+            if r == 1:
+                assert y == y0, kw
+
+
+def test_lz4_two_pass_c3_like_batch(gpu, o):
+    """A few hundred 64 KiB text bodies (the bench's C3 shape): the index
+    pass's wave-wide bitmap allocation and the execution pass's one wave per
+    message, bytes against the inputs."""
+    b = fsg.make_batch(fsg.KIND_TEXT, np.full(300, 65536, np.uint32))
+    xs = [b.item(i) for i in range(len(b))]
+    bodies = [o.compress(x) for x in xs]
+    outs, ol, st = gpu.lz4_decompress(bodies, [len(x) for x in xs])
+    assert (st == 0).all() and all(y == x for y, x in zip(outs, xs))
