@@ -51,8 +51,14 @@ namespace {
 // ---- pass 1 geometry
 constexpr u32 kL4RingChunks = 16;  // per-lane input ring: 16 chunks of 16 bytes
 constexpr u32 kL4RingDwords = 4 * kL4RingChunks;
-constexpr u32 kL4Ahead = 6;        // chunks loaded per iteration
-constexpr int kL4Steps = 24;       // half-steps (token or offset field) per iteration
+#ifndef FSG_L4_AHEAD
+#define FSG_L4_AHEAD 8
+#endif
+#ifndef FSG_L4_STEPS
+#define FSG_L4_STEPS 24
+#endif
+constexpr u32 kL4Ahead = FSG_L4_AHEAD;  // chunks loaded per iteration
+constexpr int kL4Steps = FSG_L4_STEPS;  // half-steps (token or offset field) per iteration
 constexpr u32 kL4BitGroups = 4;    // per-lane ring of 128-byte bit groups (4 words each)
 constexpr u32 kL4BitWords = 4 * kL4BitGroups;
 constexpr i32 kL4Parsing = -1;
@@ -77,14 +83,32 @@ __device__ __forceinline__ u32x4 far16(__amdgpu_buffer_rsrc_t r, u32 off) {
 
 // ===========================================================================
 // Pass 1: validate + index, one lane per message.
+//
+// One step per sequence: the lane reads the 20 ring bytes from the dword
+// holding its token (5 LDS dwords, one round trip).  When the sequence's
+// offset field and match-length byte lie within them (literals of <= 12
+// bytes: ~97% of text sequences) the whole sequence is checked and consumed
+// in that step; a longer literal leaves the lane at its offset field
+// (half = 1) for the next step, which the ring serves from wherever the
+// literal ends.  The step is straight-line code with selects: every lane
+// runs the same instructions whichever half it is in.  A 255 extension byte
+// (a literal of >= 270 or a match of >= 274 bytes) stalls the lane until the
+// end of the iteration, where its run of 255s is read from global memory.
+__device__ __forceinline__ u32 mux5(u32 d0, u32 d1, u32 d2, u32 d3, u32 d4, u32 i) {
+  const u32 a = (i & 1) ? d1 : d0;
+  const u32 b = (i & 1) ? d3 : d2;
+  const u32 c = (i & 2) ? b : a;
+  return (i & 4) ? d4 : c;
+}
+
 __global__ __launch_bounds__(64) void lz4_index_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u32 n_msgs,
     const u32* __restrict__ out_cap, u32* __restrict__ out_len, i32* __restrict__ status_out,
     u32* __restrict__ bm_counter, u32* __restrict__ bm_base_out, u32* __restrict__ hdr_out,
     u32* __restrict__ bitmap, u64 bm_capacity_words) {
-  // [dword][lane]; dword kL4RingDwords repeats dword 0 (a 4-byte read at the
-  // ring's last dword wraps)
-  __shared__ u32 ring[(kL4RingDwords + 1) * kWave];
+  // [dword][lane]; rows kL4RingDwords.. +3 repeat rows 0..3 (a 5-dword read
+  // at the ring's end wraps)
+  __shared__ u32 ring[(kL4RingDwords + 4) * kWave];
   __shared__ u32 bmr[kL4BitWords * kWave];
   const u32 lane = threadIdx.x;
   const u32 m = blockIdx.x * kWave + lane;
@@ -126,30 +150,24 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
   const u32 bal = (u32)(reinterpret_cast<uintptr_t>(bb) & 15);
   const u8* abase = bb - bal;
   const u32 last_chunk = n ? (bal + n - 1) >> 4 : 0u;
-  auto chunk = [&](u32 k) -> u32x4 {  // (k clamped to the block's chunks)
-    return *reinterpret_cast<const u32x4*>(abase + 16 * (k <= last_chunk ? k : last_chunk));
-  };
-  auto ring_write = [&](u32 k, u32x4 v) {
-    const u32 d = (k & (kL4RingChunks - 1)) * 4;
-#pragma unroll
-    for (u32 i = 0; i < 4; ++i) ring[(d + i) * kWave + lane] = v[i];
-    if (d == 0) ring[kL4RingDwords * kWave + lane] = v[0];
-  };
-  // 4 bytes at block offset p, from the ring
-  auto rd4 = [&](u32 p) -> u32 {
-    const u32 P = p + bal;
-    const u32 dw = (P >> 2) & (kL4RingDwords - 1);
-    return alignbyte(ring[(dw + 1) * kWave + lane], ring[dw * kWave + lane], P & 3);
-  };
+#define L4_CHUNK(k) (*reinterpret_cast<const u32x4*>(abase + 16 * ((k) <= last_chunk ? (k) : last_chunk)))
+#define L4_RING_WRITE(k, v)                                                             \
+  do {                                                                                  \
+    const u32 d_ = ((k) & (kL4RingChunks - 1)) * 4;                                     \
+    _Pragma("unroll") for (u32 i_ = 0; i_ < 4; ++i_) ring[(d_ + i_) * kWave + lane] = (v)[i_]; \
+    if (d_ == 0) {                                                                      \
+      _Pragma("unroll") for (u32 i_ = 0; i_ < 4; ++i_) ring[(kL4RingDwords + i_) * kWave + lane] = (v)[i_]; \
+    }                                                                                   \
+  } while (0)
 
   u32 wend = 0, iend = 0;  // chunks landed in the ring end at wend; loads issued end at iend
   if (st < 0 && n) {
     u32x4 c0[4];
 #pragma unroll
-    for (u32 c = 0; c < 4; ++c) c0[c] = chunk(c);
+    for (u32 c = 0; c < 4; ++c) c0[c] = L4_CHUNK(c);
 #pragma unroll
     for (u32 c = 0; c < 4; ++c)
-      if (c <= last_chunk) ring_write(c, c0[c]);
+      if (c <= last_chunk) L4_RING_WRITE(c, c0[c]);
     wend = iend = last_chunk + 1 < 4 ? last_chunk + 1 : 4u;
   }
 #pragma unroll
@@ -158,79 +176,77 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
   const u32 ngroups = words >> 2;
 
   // walk state: pos = the next token (half 0) or offset field (half 1)
-  u32 pos = 0, op = 0, half = 0, nib = 0;
-  bool stall = false;  // a 255 extension byte: finished from global memory below
+  u32 pos = 0, op = 0, nib = 0;
+  bool half = false, stall = false;
   u32x4 g[kL4Ahead];
 #pragma unroll
   for (u32 c = 0; c < kL4Ahead; ++c) g[c] = u32x4{0, 0, 0, 0};
   u32 gk = 0, gn = 0;
   __builtin_amdgcn_s_waitcnt(0);
 
-  // the rest of a token step once its literal length is known (shared with
-  // the stalled lanes' path): the checks of lz4o_decompress_block :179-184
-  auto token_tail = [&](u32 tokpos, u32 lit, u32 ipl, u32 tok) {
-    if (lit > n - ipl || lit > ulen - op) {
-      st = kCorrupt;
-      return;
-    }
-    atomicOr(&bmr[((tokpos >> 5) & (kL4BitWords - 1)) * kWave + lane], 1u << (tokpos & 31));
-    if ((u64)op + lit + 12 > ulen || (u64)ipl + lit + 8 > n) {  // the last sequence
-      st = (ipl + lit == n && op + lit == ulen) ? kOk : kCorrupt;
-      return;
-    }
-    op += lit;
-    nib = tok & 15;
-    pos = ipl + lit;
-    half = 1;
-  };
-
   while (__any(st < 0)) {
-    // a half-step at pos reads 4 ring bytes: pos + bal + 4 <= 16 * wend, or
+    // a step at pos reads 20 ring bytes: pos + bal + 20 <= 16 * wend, or
     // anywhere once the ring reached the block's last chunk (bytes past the
     // block are never used: every used byte is checked against n)
     u32 lim = 0;
-    if (st < 0) lim = wend > last_chunk ? 0xffffffffu : (16 * wend >= bal + 4 ? 16 * wend - bal - 4 : 0u);
+    if (st < 0) lim = wend > last_chunk ? 0xffffffffu : (16 * wend >= bal + 20 ? 16 * wend - bal - 20 : 0u);
 #pragma unroll
     for (int j = 0; j < kL4Steps; ++j) {
-      const bool look = st < 0 && !stall && (pos <= lim || (half == 0 && pos >= n));
-      const u32 w = rd4(pos);
-      if (look) {
-        if (half == 0) {
-          // token (:168-178)
-          const u32 tok = w & 0xffu, l0 = tok >> 4, b1 = (w >> 8) & 0xffu;
-          const bool lx = l0 == 15;
-          if (pos >= n || (lx && pos + 1 >= n)) {
-            st = kCorrupt;
-          } else if (lx && b1 == 255) {
-            stall = true;
-          } else {
-            token_tail(pos, l0 + (lx ? b1 : 0u), pos + 1 + (lx ? 1u : 0u), tok);
-          }
-        } else {
-          // offset field and match length (:188-202); pos + 8 <= n here
-          const u32 off = w & 0xffffu, b2 = (w >> 16) & 0xffu;
-          const bool mx = nib == 15;
-          const u32 ml = nib + 4 + (mx ? b2 : 0u);
-          if (off == 0 || off > op) {
-            st = kCorrupt;
-          } else if (mx && b2 == 255) {
-            stall = true;
-          } else if ((u64)ml + 5 > ulen - op) {
-            st = kCorrupt;
-          } else {
-            atomicOr(&bmr[((pos >> 5) & (kL4BitWords - 1)) * kWave + lane], 1u << (pos & 31));
-            op += ml;
-            pos += 2 + (mx ? 1u : 0u);
-            half = 0;
-          }
-        }
-      }
+      const bool look = st < 0 && !stall && (pos <= lim || (!half && pos >= n));
+      const u32 P = pos + bal;
+      const u32 dw = (P >> 2) & (kL4RingDwords - 1), s = P & 3;
+      const u32 D0 = ring[dw * kWave + lane], D1 = ring[(dw + 1) * kWave + lane];
+      const u32 D2 = ring[(dw + 2) * kWave + lane], D3 = ring[(dw + 3) * kWave + lane];
+      const u32 D4 = ring[(dw + 4) * kWave + lane];
+      const u32 x0 = alignbyte(D1, D0, s);
+      // the token at pos (lz4o_decompress_block :168-184)
+      const u32 tok = x0 & 0xffu, l0 = tok >> 4, b1 = (x0 >> 8) & 0xffu;
+      const bool lx = l0 == 15;
+      const u32 lit = l0 + (lx ? b1 : 0u);
+      const u32 ipl = pos + 1 + (lx ? 1u : 0u);
+      const bool slow0 = lx && b1 == 255;
+      const bool tfail = pos >= n || (lx && pos + 1 >= n) || (!slow0 && (lit > n - ipl || lit > ulen - op));
+      const bool last = (u64)op + lit + 12 > ulen || (u64)ipl + lit + 8 > n;
+      const bool last_ok = ipl + lit == n && op + lit == ulen;
+      const u32 rel = ipl + lit - pos;  // offset field - pos
+      const bool fused = s + rel <= 15;
+      // the offset field and match length (:188-202): at pos (half 1) or
+      // right after the literal (a fused step); q + 8 <= n there
+      const u32 k = half ? s : s + rel;
+      const u32 kd = k >> 2;
+      const u32 w = alignbyte(mux5(D0, D1, D2, D3, D4, kd + 1), mux5(D0, D1, D2, D3, D4, kd), k & 3);
+      const u32 off = w & 0xffffu, b2 = (w >> 16) & 0xffu;
+      const u32 nv = half ? nib : (tok & 15);
+      const u32 opb = half ? op : op + lit;
+      const u32 qpos = half ? pos : pos + rel;
+      const bool mx = nv == 15;
+      const u32 ml = nv + 4 + (mx ? b2 : 0u);
+      const bool slow1 = mx && b2 == 255;
+      const bool mfail = off == 0 || off > opb || (!slow1 && (u64)ml + 5 > ulen - opb);
+      // outcomes
+      const bool tstage = look && !half;
+      const bool t_ok = tstage && !tfail && !slow0;  // token accepted: its bit
+      const bool mstage = look && (half || (t_ok && !last && fused));
+      const bool m_ok = mstage && !mfail && !slow1;   // match accepted: the offset field's bit
+      const bool m_stall = mstage && !mfail && slow1;
+      atomicOr(&bmr[((pos >> 5) & (kL4BitWords - 1)) * kWave + lane], t_ok ? 1u << (pos & 31) : 0u);
+      atomicOr(&bmr[((qpos >> 5) & (kL4BitWords - 1)) * kWave + lane], m_ok ? 1u << (qpos & 31) : 0u);
+      i32 nst = st;
+      nst = (tstage && tfail) || (mstage && mfail) ? kCorrupt : nst;
+      nst = t_ok && last ? (last_ok ? kOk : kCorrupt) : nst;
+      st = nst;
+      stall = stall || (tstage && !tfail && slow0) || m_stall;
+      const bool to_half1 = (t_ok && !last && !fused) || m_stall;
+      pos = m_ok ? qpos + 2 + (mx ? 1u : 0u) : (to_half1 ? qpos : pos);
+      op = m_ok ? opb + ml : (to_half1 ? opb : op);
+      nib = to_half1 ? nv : nib;
+      half = m_ok ? false : (to_half1 ? true : half);
     }
     // ---------- stalled lanes: extension runs of 255s, from global memory
     if (stall && st < 0) {
       stall = false;
-      if (half == 0) {
-        u32 p = pos + 2, lit = 15 + 255, b;
+      if (!half) {  // a literal length: 15 + 255 + ... from pos + 2
+        u32 p = pos + 2, lit = 15 + 255, b = 255;
         bool bad = false;
         do {
           if (p >= n) {
@@ -240,10 +256,21 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
           b = bb[p++];
           lit += b;
         } while (b == 255 && lit <= n);  // (lit > n fails the next check either way)
-        if (bad) st = kCorrupt;
-        else token_tail(pos, lit, p, (u32)bb[pos]);
-      } else {
-        u32 p = pos + 3, ml = 15 + 4 + 255, b;
+        if (bad || lit > n - p || lit > ulen - op) {
+          st = kCorrupt;
+        } else {
+          atomicOr(&bmr[((pos >> 5) & (kL4BitWords - 1)) * kWave + lane], 1u << (pos & 31));
+          if ((u64)op + lit + 12 > ulen || (u64)p + lit + 8 > n) {  // the last sequence
+            st = (p + lit == n && op + lit == ulen) ? kOk : kCorrupt;
+          } else {
+            op += lit;
+            nib = bb[pos] & 15;
+            pos = p + lit;
+            half = true;
+          }
+        }
+      } else {  // a match length: 19 + 255 + ... from pos + 3 (offset checked)
+        u32 p = pos + 3, ml = 15 + 4 + 255, b = 255;
         bool bad = false;
         do {
           if (p >= n) {
@@ -259,7 +286,7 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
           atomicOr(&bmr[((pos >> 5) & (kL4BitWords - 1)) * kWave + lane], 1u << (pos & 31));
           op += ml;
           pos = p;
-          half = 0;
+          half = false;
         }
       }
     }
@@ -269,8 +296,8 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
     if (st < 0 || st == kOk) {
       const u32 cur = st < 0 ? pos >> 7 : ngroups;
 #pragma unroll
-      for (u32 k = 0; k < kL4BitGroups; ++k) {
-        const u32 gi = fg + k;
+      for (u32 kk = 0; kk < kL4BitGroups; ++kk) {
+        const u32 gi = fg + kk;
         if (gi < cur) {
           const u32 sl = (gi & (kL4BitGroups - 1)) * 4;
           u32x4 v;
@@ -288,7 +315,7 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
     // ---------- land last iteration's chunks, load the next ones
 #pragma unroll
     for (u32 c = 0; c < kL4Ahead; ++c)
-      if (c < gn) ring_write(gk + c, g[c]);
+      if (c < gn) L4_RING_WRITE(gk + c, g[c]);
     wend = gn ? gk + gn : wend;
     gn = 0;
     if (st < 0) {
@@ -297,14 +324,16 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
       if (pc >= iend) wend = pc;                // (nothing at or above pc is landed)
 #pragma unroll
       for (u32 c = 0; c < kL4Ahead; ++c) {
-        const u32 k = base + c;
-        gn += (k <= last_chunk && k <= pc + (kL4RingChunks - 1)) ? 1u : 0u;
-        g[c] = chunk(k);
+        const u32 kc = base + c;
+        gn += (kc <= last_chunk && kc <= pc + (kL4RingChunks - 1)) ? 1u : 0u;
+        g[c] = L4_CHUNK(kc);
       }
       gk = base;
       iend = base + gn > iend ? base + gn : iend;
     }
   }
+#undef L4_CHUNK
+#undef L4_RING_WRITE
   if (valid) status_out[m] = st;
 }
 

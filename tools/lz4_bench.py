@@ -59,18 +59,21 @@ def main():
     def dec2():  # the two-pass decoder (fsg_lz4_decompress_batch_ws)
         codec.lz4_decompress(d_c, d_co, d_cl, n, d_out, d_ro, d_rl, d_ol, d_st, stream=s, workspace=dws)
 
-    def timed(fn):
+    def timed(fn, steps=None):
+        steps = a.steps if steps is None else steps
         fn()
         torch.cuda.synchronize()
+        if steps == 0:
+            return float("nan")
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(s)
-        for _ in range(a.steps):
+        for _ in range(steps):
             fn()
         e1.record(s)
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / a.steps
+        return e0.elapsed_time(e1) / steps
 
-    enc_ms = timed(enc)
+    enc_ms = timed(enc, 0 if a.two_pass_only else None)
     comp_len = d_cl.cpu().numpy().view(np.uint32)
     comp = int(comp_len.astype(np.uint64).sum())
     enc_ok = int((d_st != 0).sum().item()) == 0
