@@ -467,7 +467,7 @@ def rank_main(args, codec_factory=None):
         value = raw_all / t_step / GIB
         achieved = algo_bytes / avg_kernel_s / 1e9
         # PMC traffic is per launch of the full-size workload on one rank's shard
-        pmc = load_traffic(args.workload) if (args.n_msgs == 0 and scaling == "weak") else None
+        pmc = load_traffic(args.workload) if (args.n_msgs == 0 and (scaling == "weak" or world == 1)) else None
         line = {
             "metric": METRIC,
             "value": round(value, 3),

@@ -65,9 +65,28 @@ constexpr i32 kL4Parsing = -1;
 
 // ---- pass 2 geometry
 constexpr u32 kL4Waves = 4;                   // waves per block
-constexpr u32 kL4Ring = 512;                  // bitmap positions per wave
-constexpr u32 kL4FillWords = kL4Ring / 32;    // <= 512 bits: <= 342 positions (two per three bytes)
-constexpr u32 kL4Window = 3072;               // LDS output window per wave
+// The ring is refilled while it holds fewer than kL4RefillBelow positions; a
+// fill adds <= 512 bits = <= 342 positions (two per three bytes).  With 1,024
+// positions and a refill below 260, the next group's prefetch (issued at the
+// end of this one) always finds its positions in the ring; measured slower
+// on C3 than 512 / 130 all the same (6.66 vs 6.37 ms, A/B on one box, the
+// larger ring costing a wave per SIMD), as were four round-A chunks per pass
+// (6.95 vs 6.37: 84 VGPRs) and a 2,560-byte window (6.85).
+#ifndef FSG_L4_RING
+#define FSG_L4_RING 512
+#endif
+#ifndef FSG_L4_ITEMS
+#define FSG_L4_ITEMS 2
+#endif
+constexpr u32 kL4Ring = FSG_L4_RING;          // bitmap positions per wave
+constexpr u32 kL4FillWords = 16;
+constexpr u32 kL4RefillBelow = kL4Ring >= 1024 ? 2 * (2 * 64 + 1) + 2 : 2 * 64 + 2;
+static_assert(kL4RefillBelow + 342 <= kL4Ring, "a fill fits the ring");
+constexpr u32 kL4ItemsPerPass = FSG_L4_ITEMS;  // round-A chunks per lane per round trip
+#ifndef FSG_L4_WINDOW
+#define FSG_L4_WINDOW 3072
+#endif
+constexpr u32 kL4Window = FSG_L4_WINDOW;      // LDS output window per wave
 constexpr u32 kL4Keep = 1024;                 // history kept when it slides
 constexpr u32 kL4GroupBytes = 1024;           // output bytes per group
 constexpr u32 kL4Long = 64;                   // longer literal or match: whole-wave sequence
@@ -403,7 +422,7 @@ __device__ __forceinline__ void lz4_exec_message(
 
   for (;;) {
     // ---------- refill the position ring (a group needs 2 * 64 + 1 entries)
-    if (tail - head < 2 * 64 + 2 && scan < nwords) {
+    if (tail - head < kL4RefillBelow && scan < nwords) {
       u32 bits = (bmw >> (8 * (lane & 3))) & 0xffu;
       const u32 bitbase = (scan + (lane >> 2)) * 32 + 8 * (lane & 3);
       const u32 cnt = __builtin_popcount(bits);
@@ -610,7 +629,9 @@ __device__ __forceinline__ void lz4_exec_message(
     const bool reg0 = lit <= 14;
     const u32 wa = (u32)((int)t_op - sbase);
     const u32 wm = wa + lit;
-    // items: literal chunks [0, nlc), then far chunks [0, kc); two per pass
+    // items: literal chunks [0, nlc), then far chunks [0, kc); four per pass
+    // (one round trip unless a lane has a literal over 48 bytes with a far
+    // chunk, or more)
     const u32 nit = nlc + kc;
     // the previous groups' completed blocks, 1 KiB at a time
     auto flush_group = [&]() {
@@ -618,10 +639,16 @@ __device__ __forceinline__ void lz4_exec_message(
       if (fe >= (int)flushed + 1024) flush_to((u32)fe);
     };
     if (!__ballot(nit > 0)) flush_group();
-    for (u32 i0 = 0; __ballot(i0 < nit); i0 += 2) {
-      u32x4 x0 = u32x4{0, 0, 0, 0}, x1 = u32x4{0, 0, 0, 0};
-      u32 y0 = 0, y1 = 0;
-      bool l0 = false, l1 = false;  // item is a literal chunk
+    for (u32 i0 = 0; __ballot(i0 < nit); i0 += kL4ItemsPerPass) {
+      u32x4 xs[kL4ItemsPerPass];
+      u32 ys[kL4ItemsPerPass];
+      bool ls[kL4ItemsPerPass];  // item is a literal chunk
+#pragma unroll
+      for (u32 r = 0; r < kL4ItemsPerPass; ++r) {
+        xs[r] = u32x4{0, 0, 0, 0};
+        ys[r] = 0;
+        ls[r] = false;
+      }
       auto issue = [&](u32 it, u32x4& x, u32& y, bool& isl) {
         if (it >= nit) return;
         if (it < nlc) {
@@ -638,8 +665,8 @@ __device__ __forceinline__ void lz4_exec_message(
           x = far16(orsrc, mo + 16 * (it - nlc) + obal);
         }
       };
-      issue(i0, x0, y0, l0);
-      issue(i0 + 1, x1, y1, l1);
+#pragma unroll
+      for (u32 r = 0; r < kL4ItemsPerPass; ++r) issue(i0 + r, xs[r], ys[r], ls[r]);
       if (i0 == 0) flush_group();  // while the loads are in flight
       auto land = [&](u32 it, u32x4 x, u32 y, bool isl) {
         if (it >= nit) return;
@@ -657,8 +684,8 @@ __device__ __forceinline__ void lz4_exec_message(
           or_store(sb, wm + 16 * k, x, r < 16 ? r : 16u, mtab);
         }
       };
-      land(i0, x0, y0, l0);
-      land(i0 + 1, x1, y1, l1);
+#pragma unroll
+      for (u32 r = 0; r < kL4ItemsPerPass; ++r) land(i0 + r, xs[r], ys[r], ls[r]);
     }
     wave_lds_fence();
 
