@@ -113,11 +113,10 @@ __device__ __forceinline__ u32x4 far16(__amdgpu_buffer_rsrc_t r, u32 off) {
 // runs the same instructions whichever half it is in.  A 255 extension byte
 // (a literal of >= 270 or a match of >= 274 bytes) stalls the lane until the
 // end of the iteration, where its run of 255s is read from global memory.
-__device__ __forceinline__ u32 mux5(u32 d0, u32 d1, u32 d2, u32 d3, u32 d4, u32 i) {
+__device__ __forceinline__ u32 mux4(u32 d0, u32 d1, u32 d2, u32 d3, u32 i) {
   const u32 a = (i & 1) ? d1 : d0;
   const u32 b = (i & 1) ? d3 : d2;
-  const u32 c = (i & 2) ? b : a;
-  return (i & 4) ? d4 : c;
+  return (i & 2) ? b : a;
 }
 
 __global__ __launch_bounds__(64) void lz4_index_kernel(
@@ -224,16 +223,20 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
       const u32 lit = l0 + (lx ? b1 : 0u);
       const u32 ipl = pos + 1 + (lx ? 1u : 0u);
       const bool slow0 = lx && b1 == 255;
-      const bool tfail = pos >= n || (lx && pos + 1 >= n) || (!slow0 && (lit > n - ipl || lit > ulen - op));
-      const bool last = (u64)op + lit + 12 > ulen || (u64)ipl + lit + 8 > n;
+      // (bitwise, not short-circuit: no branch in the unrolled walk; when
+      // pos >= n the wrapped differences are never the deciding term)
+      const u32 room = (n - ipl) < (ulen - op) ? (n - ipl) : (ulen - op);
+      const bool tfail = (pos >= n) | (lx & (pos + 1 >= n)) | (!slow0 & (lit > room));
+      // (u32: op <= ulen always; ipl <= n unless tfail)
+      const bool last = lit + 12 > ulen - op || lit + 8 > n - ipl;
       const bool last_ok = ipl + lit == n && op + lit == ulen;
       const u32 rel = ipl + lit - pos;  // offset field - pos
       const bool fused = s + rel <= 15;
       // the offset field and match length (:188-202): at pos (half 1) or
       // right after the literal (a fused step); q + 8 <= n there
-      const u32 k = half ? s : s + rel;
+      const u32 k = half ? s : s + rel;  // <= 15 whenever used
       const u32 kd = k >> 2;
-      const u32 w = alignbyte(mux5(D0, D1, D2, D3, D4, kd + 1), mux5(D0, D1, D2, D3, D4, kd), k & 3);
+      const u32 w = alignbyte(mux4(D1, D2, D3, D4, kd), mux4(D0, D1, D2, D3, kd), k & 3);
       const u32 off = w & 0xffffu, b2 = (w >> 16) & 0xffu;
       const u32 nv = half ? nib : (tok & 15);
       const u32 opb = half ? op : op + lit;
@@ -241,7 +244,7 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
       const bool mx = nv == 15;
       const u32 ml = nv + 4 + (mx ? b2 : 0u);
       const bool slow1 = mx && b2 == 255;
-      const bool mfail = off == 0 || off > opb || (!slow1 && (u64)ml + 5 > ulen - opb);
+      const bool mfail = off == 0 || off > opb || (!slow1 && ml + 5 > ulen - opb);  // (opb <= ulen unless tfail)
       // outcomes
       const bool tstage = look && !half;
       const bool t_ok = tstage && !tfail && !slow0;  // token accepted: its bit
