@@ -423,23 +423,28 @@ __device__ __forceinline__ void lz4_exec_message(
     flushed = fe;
   };
 
+  // one fill: kL4FillWords bitmap words (prefetched in bmw) into the ring
+  auto fill = [&]() {
+    u32 bits = (bmw >> (8 * (lane & 3))) & 0xffu;
+    const u32 bitbase = (scan + (lane >> 2)) * 32 + 8 * (lane & 3);
+    const u32 cnt = __builtin_popcount(bits);
+    const u32 inc = dpp_incl_scan(cnt);
+    u32 slot = tail + inc - cnt;
+    while (bits) {
+      ring[slot & M] = bitbase + __builtin_ctz(bits);
+      ++slot;
+      bits &= bits - 1;
+    }
+    tail += readlane(inc, 63);
+    scan += kL4FillWords;
+    bmw = fill_word(scan);
+    wave_lds_fence();
+  };
+
   for (;;) {
     // ---------- refill the position ring (a group needs 2 * 64 + 1 entries)
     if (tail - head < kL4RefillBelow && scan < nwords) {
-      u32 bits = (bmw >> (8 * (lane & 3))) & 0xffu;
-      const u32 bitbase = (scan + (lane >> 2)) * 32 + 8 * (lane & 3);
-      const u32 cnt = __builtin_popcount(bits);
-      const u32 inc = dpp_incl_scan(cnt);
-      u32 slot = tail + inc - cnt;
-      while (bits) {
-        ring[slot & M] = bitbase + __builtin_ctz(bits);
-        ++slot;
-        bits &= bits - 1;
-      }
-      tail += readlane(inc, 63);
-      scan += kL4FillWords;
-      bmw = fill_word(scan);
-      wave_lds_fence();
+      fill();
       continue;
     }
     const u32 avail = tail - head;
@@ -604,9 +609,14 @@ __device__ __forceinline__ void lz4_exec_message(
       sbase = nsb;
       zero_end = (keep + 15) & ~15u;
     }
-    // ---------- prefetch the next group
+    // ---------- prefetch the next group; the ring is refilled first when
+    // the next group would find it short (a fill writes slots below nh only:
+    // tail - nh < kL4RefillBelow and a fill adds <= 342), so the prefetch
+    // covers all of that group's positions (else the group reloads them
+    // itself, one exposed round trip)
     {
       const u32 nh = head + 2 * k_seq;
+      if (tail - nh < kL4RefillBelow && scan < nwords) fill();
       const u32 nT = ring[(nh + 2 * lane) & M];
       const u32 nO = ring[(nh + 2 * lane + 1) & M];
       prefetch(nT, nO);
@@ -628,67 +638,62 @@ __device__ __forceinline__ void lz4_exec_message(
     const u32 below = (u32)(sbase - (int)mo);
     const u32 kfar = (int)below > 0 ? ((below - 1) >> 4) + 1 : 0u;
     const u32 kc = (!fits || is_last || pat) ? 0u : (kfar < nch ? kfar : nch);
-    const u32 nlc = fits ? (lit + 15) >> 4 : 0u;
-    const bool reg0 = lit <= 14;
+    // a literal of <= 14 bytes comes from the prefetched token bytes; a
+    // longer one in 16-byte chunks from the input
+    const bool regl = fits && lit > 0 && lit <= 14;
+    const u32 nlm = (fits && lit > 14) ? (lit + 15) >> 4 : 0u;
     const u32 wa = (u32)((int)t_op - sbase);
     const u32 wm = wa + lit;
-    // items: literal chunks [0, nlc), then far chunks [0, kc); four per pass
-    // (one round trip unless a lane has a literal over 48 bytes with a far
-    // chunk, or more)
-    const u32 nit = nlc + kc;
+    // load items: input literal chunks [0, nlm), then far chunks [0, kc); two
+    // per round trip
+    const u32 nit = nlm + kc;
     // the previous groups' completed blocks, 1 KiB at a time
     auto flush_group = [&]() {
       const int fe = (int)((op + obal) & ~15u) - (int)obal;
       if (fe >= (int)flushed + 1024) flush_to((u32)fe);
     };
-    if (!__ballot(nit > 0)) flush_group();
+    if (!__ballot(nit > 0)) {
+      flush_group();
+      if (regl) or_store(sb, wa, xr, lit, mtab);
+    }
     for (u32 i0 = 0; __ballot(i0 < nit); i0 += kL4ItemsPerPass) {
       u32x4 xs[kL4ItemsPerPass];
       u32 ys[kL4ItemsPerPass];
-      bool ls[kL4ItemsPerPass];  // item is a literal chunk
 #pragma unroll
       for (u32 r = 0; r < kL4ItemsPerPass; ++r) {
         xs[r] = u32x4{0, 0, 0, 0};
         ys[r] = 0;
-        ls[r] = false;
       }
-      auto issue = [&](u32 it, u32x4& x, u32& y, bool& isl) {
-        if (it >= nit) return;
-        if (it < nlc) {
-          isl = true;
-          if (it == 0 && reg0) {
-            x = xr;
-            y = 0xffffffffu;  // marker: already shifted
-          } else {
-            const u32 a = (lsrc + 16 * it + bbal) & ~3u;
-            x = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
-            y = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
-          }
-        } else {
-          x = far16(orsrc, mo + 16 * (it - nlc) + obal);
-        }
-      };
 #pragma unroll
-      for (u32 r = 0; r < kL4ItemsPerPass; ++r) issue(i0 + r, xs[r], ys[r], ls[r]);
-      if (i0 == 0) flush_group();  // while the loads are in flight
-      auto land = [&](u32 it, u32x4 x, u32 y, bool isl) {
-        if (it >= nit) return;
-        if (isl) {
-          if (!(it == 0 && reg0)) {
-            const u32 sh = (lsrc + 16 * it + bbal) & 3u;
-            x = u32x4{alignbyte(x[1], x[0], sh), alignbyte(x[2], x[1], sh), alignbyte(x[3], x[2], sh),
-                      alignbyte(y, x[3], sh)};
-          }
-          const u32 r = lit - 16 * it;
-          or_store(sb, wa + 16 * it, x, r < 16 ? r : 16u, mtab);
-        } else {
-          const u32 k = it - nlc;
-          const u32 r = ml - 16 * k;
-          or_store(sb, wm + 16 * k, x, r < 16 ? r : 16u, mtab);
+      for (u32 r = 0; r < kL4ItemsPerPass; ++r) {
+        const u32 it = i0 + r;
+        if (it < nlm) {
+          const u32 a = (lsrc + 16 * it + bbal) & ~3u;
+          xs[r] = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
+          ys[r] = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
+        } else if (it < nit) {
+          xs[r] = far16(orsrc, mo + 16 * (it - nlm) + obal);
         }
-      };
+      }
+      if (i0 == 0) {  // while the loads are in flight
+        flush_group();
+        if (regl) or_store(sb, wa, xr, lit, mtab);
+      }
 #pragma unroll
-      for (u32 r = 0; r < kL4ItemsPerPass; ++r) land(i0 + r, xs[r], ys[r], ls[r]);
+      for (u32 r = 0; r < kL4ItemsPerPass; ++r) {
+        const u32 it = i0 + r;
+        if (it < nlm) {
+          const u32 sh = (lsrc + 16 * it + bbal) & 3u;
+          const u32x4 x = u32x4{alignbyte(xs[r][1], xs[r][0], sh), alignbyte(xs[r][2], xs[r][1], sh),
+                                alignbyte(xs[r][3], xs[r][2], sh), alignbyte(ys[r], xs[r][3], sh)};
+          const u32 rr = lit - 16 * it;
+          or_store(sb, wa + 16 * it, x, rr < 16 ? rr : 16u, mtab);
+        } else if (it < nit) {
+          const u32 k = it - nlm;
+          const u32 rr = ml - 16 * k;
+          or_store(sb, wm + 16 * k, xs[r], rr < 16 ? rr : 16u, mtab);
+        }
+      }
     }
     wave_lds_fence();
 
