@@ -70,7 +70,6 @@ constexpr int kIdxTagsOne = 32, kIdxTagsPlanned = 24;
 #define FSG_ROUNDS_V2 1
 #endif
 constexpr u32 kRingChunks = 16;              // 16-byte chunks per lane (256 B)
-constexpr u32 kRingDwords = kRingChunks * 4;
 constexpr u32 kAhead = 7;                    // chunks prefetched per iteration
 // Waves per pass-1 workgroup.  One: most resident waves for large batches
 // (CM 15.1 ms vs 17.9 with four).  Four (82 KB of LDS: one workgroup per CU,
@@ -2348,7 +2347,7 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     u32* __restrict__ bitmap, const u32* __restrict__ seg_list,
     const u32* __restrict__ seg_count, const u32* __restrict__ whole_list,
     const u32* __restrict__ whole_count, u32* __restrict__ exec_next, u32 big_blocks,
-    u32 big_threshold, u32 prio, u32 keep_hist) {
+    u32 big_threshold, u32 prio, u32 keep_hist, u32 small_stride) {
   // per wave: the tag ring, then the output window
   __shared__ __attribute__((aligned(16))) u8 wl_s[kWavesPerBlock][4 * kTagRing + kWindow + 32];
   __shared__ __attribute__((aligned(16))) u8 pmap_s[kWavesPerBlock][V == 5 ? 1 : kMaxPieces];
@@ -2381,8 +2380,14 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
   u8* sb = wl_s[wv] + 4 * kTagRing;
 
   if (blockIdx.x >= big_blocks) {
-    const u32 m = (blockIdx.x - big_blocks) * kWavesPerBlock + wv;
-    if (m < n_msgs && in_len[m] <= big_threshold) run(m, ring, pmap, sb, lane, status[m], 0u, 0u, out_len[m]);
+    // one message per wave; or, with small_stride (blocks), every
+    // small_stride-th group of kWavesPerBlock messages: a wave runs many
+    // small messages, paying its launch and the block's table set-up once
+    // (the forked path's batches of mostly small bodies)
+    const u32 m0 = (blockIdx.x - big_blocks) * kWavesPerBlock + wv;
+    const u32 step = small_stride ? small_stride * kWavesPerBlock : 0xffffffffu;
+    for (u32 m = m0; m < n_msgs; m = m + step < m ? 0xffffffffu : m + step)
+      if (in_len[m] <= big_threshold) run(m, ring, pmap, sb, lane, status[m], 0u, 0u, out_len[m]);
     return;
   }
   // large messages, listed by pass 1b: whole ones first (the longest start
@@ -2735,7 +2740,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     ek<<<fork_big_blocks, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(b.seg_list), b.seg_count, b.whole_list, b.whole_count, b.exec_next,
-        fork_big_blocks, big_threshold, 0u, keep_hist);
+        fork_big_blocks, big_threshold, 0u, keep_hist, 0u);
     return hipGetLastError();
   };
   // The huge messages' pass 1b, chunked (chunk_*_kernel): when the record
@@ -2775,16 +2780,26 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     ek<<<fork_big_blocks, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(b.seg_list), b.seg_count, b.whole_list, b.whole_count, b.exec_next,
-        fork_big_blocks, big_threshold, 0u, keep_hist);
+        fork_big_blocks, big_threshold, 0u, keep_hist, 0u);
     return hipGetLastError();
   };
+  // The forked path's small-message launch: a grid of kSmallPersist blocks
+  // (7 waves per SIMD), each wave looping over messages; CM 7.31 -> 7.02 ms
+  // against one wave per message (A/B on one box, two passes; 1,024 blocks:
+  // 7.11, 3,584: 7.03).  FSG_SMALL_PERSIST (blocks, read per call: the tests
+  // shrink it; 0 = one wave per message).
+  const u32 kSmallPersist = [] {
+    const char* e = getenv("FSG_SMALL_PERSIST");
+    return e ? (u32)atoi(e) : 1792u;
+  }();
   auto launch_small = [&](hipStream_t st) -> hipError_t {
     // one wave per message; large ones are skipped (big_blocks = 0: no block
     // takes the large-message role)
-    ek<<<small_blocks, kWavesPerBlock * 64, 0, st>>>(
+    const u32 grid = kSmallPersist && kSmallPersist < small_blocks ? kSmallPersist : small_blocks;
+    ek<<<grid, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), set0.seg_count, whole_list, set0.whole_count, set0.exec_next,
-        0u, big_threshold, 0u, keep_hist);
+        0u, big_threshold, 0u, keep_hist, grid < small_blocks ? grid : 0u);
     return hipGetLastError();
   };
   SideStream* side = fork ? side_stream() : nullptr;
@@ -2836,7 +2851,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     ek<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), set0.seg_count, whole_list, set0.whole_count, set0.exec_next,
-        big_blocks, big_threshold, kPrio, keep_hist);
+        big_blocks, big_threshold, kPrio, keep_hist, 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // Diagnostic only (FSG_DIAG_NO_TAIL=1): skip this pass to trace the

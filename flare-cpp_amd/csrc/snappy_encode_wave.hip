@@ -113,19 +113,6 @@ __device__ __forceinline__ u32 incl_scan64(u32 v) {
   return r;
 }
 
-// Byte-exact store of the low nb (1..4) bytes of v (one lane).
-__device__ __forceinline__ void st_bytes(u8* p, u32 v, u32 nb) {
-  if (nb == 4) {
-    __builtin_memcpy(p, &v, 4);
-  } else {
-    if (nb & 2) {
-      const u16 s = (u16)v;
-      __builtin_memcpy(p, &s, 2);
-    }
-    if (nb & 1) p[nb - 1] = (u8)(v >> (8 * (nb - 1)));
-  }
-}
-
 // EmitCopyLessThan64 (snappy.cc:198-214) as packed bytes; *nb = 2 or 3.
 __device__ __forceinline__ u32 copy_tag(u32 offset, u32 len, u32* nb) {
   if (len < 12 && offset < 2048) {
@@ -402,8 +389,6 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       const u32 p1 = pscr[lane];
       const u32 t2 = bperm(p1, p1 & 63);
       const u32 p2 = p1 < 64 ? t2 : p1;
-      const u32 t3 = bperm(p1, p2 & 63);
-      const u32 p3 = p2 < 64 ? t3 : p2;
       const u32 X1 = bperm(X, p1 & 63);
       W5 w1;
 #pragma unroll
@@ -419,7 +404,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       // work on these masks; only lanes with a predecessor below the first
       // T-match are looked at one by one.
       const u64 HasP = __ballot(p1 < 64), Unk = __ballot(p1 == kPredUnknown);
-      const u64 MTb = __ballot(mT), M1b = __ballot(X == X1);
+      const u64 MTb = __ballot(mT);
       const u64 Deep = __ballot(p1 < 64 && p2 != kPredNone);  // a second predecessor below
       const u64 Stat = ~(HasP | Unk);
       STAMP(2);

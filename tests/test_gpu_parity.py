@@ -123,12 +123,15 @@ def test_randomized_against_oracle(gpu, oracle, encoder):
     assert (st == 0).all() and all(o == x for o, x in zip(outs, items))
 
 
-@pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1")])
+@pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1"), (0, "1p")])
 def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, monkeypatch):
     """Mutated and truncated streams (64 B to 70 KB bodies).  fork "1" runs
     the path of batches over 128K messages: plan pass, side stream, and
-    bodies of <= 1 KiB output decoded one per lane."""
-    monkeypatch.setenv("FSG_DECODE_FORK", fork)
+    bodies of <= 1 KiB output decoded one per lane; "1p" with the small
+    messages' execution grid shrunk to 5 blocks, so each wave loops over
+    ~150 messages (FSG_SMALL_PERSIST)."""
+    monkeypatch.setenv("FSG_DECODE_FORK", fork[0])
+    monkeypatch.setenv("FSG_SMALL_PERSIST", "5" if fork == "1p" else "1792")
     gpu.codec.select_kernels(variant, 0)
     rng = np.random.default_rng(9)
     srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (64, 700, 9000, 70000)]
@@ -629,7 +632,7 @@ def test_two_stream_decode_stream_of_batches(gpu, oracle):
                 assert outs[i][:ulen] == ref, (k, i)
 
 
-@pytest.mark.parametrize("fork", ["0", "1"])
+@pytest.mark.parametrize("fork", ["0", "1", "1p"])
 @pytest.mark.parametrize("fill", [0xFF, 0x5A])
 def test_decode_with_garbage_workspace(gpu, oracle, fork, fill, monkeypatch):
     """The launch zeroes only the workspace's counters and lists: the index
@@ -638,7 +641,8 @@ def test_decode_with_garbage_workspace(gpu, oracle, fork, fill, monkeypatch):
     pass 1b its whole message).  Decode with the workspace filled with
     garbage: text of many sizes, long literals inside text, single-literal
     and large (pass 1b) bodies, intact and corrupted, against the oracle."""
-    monkeypatch.setenv("FSG_DECODE_FORK", fork)
+    monkeypatch.setenv("FSG_DECODE_FORK", fork[0])
+    monkeypatch.setenv("FSG_SMALL_PERSIST", "3" if fork == "1p" else "1792")
     rng = np.random.default_rng(fill)
     srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0)
             for s in (1, 33, 200, 1000, 4096, 9000, 65536, 70000, 200000)]
