@@ -93,6 +93,23 @@ constexpr u32 kL4Long = 64;                   // longer literal or match: whole-
 constexpr u32 kL4StageMax = (kL4Window + 32) / 2 - 16;  // period staged in LDS (long overlapping match)
 static_assert(kL4Keep + kL4GroupBytes + 48 <= kL4Window, "a group fits the window after a slide");
 
+// Diagnostic build only (-DFSG_STAMPS): per-phase cycle totals of
+// lz4_exec_kernel summed over waves (slots 0-5), groups (6) and rounds-B
+// iterations (7); read back with fsg_debug_l4stamps (tools/stamps.py lz4).
+#ifdef FSG_STAMPS
+__device__ unsigned long long g_l4_stamps[8];
+#define L4STAMP(k)                                    \
+  do {                                                \
+    const u64 t_ = __builtin_amdgcn_s_memtime();      \
+    st_[k] += t_ - t_last_;                           \
+    t_last_ = t_;                                     \
+  } while (0)
+#define L4COUNT(k) (st_[k] += 1)
+#else
+#define L4STAMP(k) do { } while (0)
+#define L4COUNT(k) do { } while (0)
+#endif
+
 // Far chunks: earlier output of this wave, read through the slot's buffer
 // with an sc1 load (served by L2; the CU's L1 may hold a line filled before
 // the bytes were stored -- see snappy_decode_v4.hip, far_load).
@@ -395,6 +412,10 @@ __device__ __forceinline__ void lz4_exec_message(
     return (lane < 4 * kL4FillWords && wi < nwords) ? bm[wi] : 0u;
   };
   u32 bmw = fill_word(scan);
+#ifdef FSG_STAMPS
+  u64 st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 t_last_ = __builtin_amdgcn_s_memtime();
+#endif
   // prefetched per lane for the group at pf_head: 20 bytes from the dword
   // below the token, 8 from the dword below the offset field
   u32 pf_head = 0xffffffffu, pf_tail = 0;  // (entries at or above pf_tail were not in the ring yet)
@@ -445,6 +466,7 @@ __device__ __forceinline__ void lz4_exec_message(
     // ---------- refill the position ring (a group needs 2 * 64 + 1 entries)
     if (tail - head < kL4RefillBelow && scan < nwords) {
       fill();
+      L4STAMP(0);
       continue;
     }
     const u32 avail = tail - head;
@@ -477,6 +499,7 @@ __device__ __forceinline__ void lz4_exec_message(
     const u32 ml = is_last ? 0u : (E == 0 ? (tok & 15) + 4 : 19 + ((ow >> 16) & 0xffu));
     const bool lng = valid && (lit > kL4Long || ml > kL4Long || (!is_last && E >= 2));
     const u64 bigm = __ballot(lng);
+    L4STAMP(1);
 
     if (bigm & 1ull) {
       // ---------- a long sequence: the whole wave, straight to the slot
@@ -577,6 +600,7 @@ __device__ __forceinline__ void lz4_exec_message(
           bmw = fill_word(scan);
         }
       }
+      L4STAMP(2);
       continue;
     }
     const u32 take = bigm ? (u32)__builtin_ctzll(bigm) : kseq;
@@ -628,6 +652,7 @@ __device__ __forceinline__ void lz4_exec_message(
       zero_end += 1024;
     }
     wave_lds_fence();
+    L4STAMP(3);
 
     // ---------- round A: literals (registers for <= 14 bytes, else the
     // input) and the match's leading chunks whose source starts below the
@@ -696,6 +721,7 @@ __device__ __forceinline__ void lz4_exec_message(
       }
     }
     wave_lds_fence();
+    L4STAMP(4);
 
     // ---------- rounds B: the near match chunks in dependency order (as the
     // Snappy pass 2: a chunk runs once its source ends at or below the first
@@ -730,14 +756,24 @@ __device__ __forceinline__ void lz4_exec_message(
       }
       wave_lds_fence();
       pend = __ballot(rem > 0);
+      L4COUNT(7);
     }
     op += tot;
     head += group_last ? 2 * k_seq - 1 : 2 * k_seq;
+    L4STAMP(5);
+    L4COUNT(6);
   }
   flush_to(expected);
+#ifdef FSG_STAMPS
+  if (lane == 0)
+    for (int k = 0; k < 8; ++k) atomicAdd(&g_l4_stamps[k], (unsigned long long)st_[k]);
+#endif
 }
 
-__global__ __launch_bounds__(kL4Waves * 64) void lz4_exec_kernel(
+#ifndef FSG_L4_EXEC_WAVES
+#define FSG_L4_EXEC_WAVES 7
+#endif
+__global__ __launch_bounds__(kL4Waves * 64) __attribute__((amdgpu_waves_per_eu(FSG_L4_EXEC_WAVES, FSG_L4_EXEC_WAVES))) void lz4_exec_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u32 n_msgs,
     u8* out, const u64* __restrict__ out_off, const u32* __restrict__ out_len, const i32* __restrict__ status,
     const u32* __restrict__ bm_base, const u32* __restrict__ hdr, const u32* __restrict__ bitmap) {
@@ -756,6 +792,17 @@ __global__ __launch_bounds__(kL4Waves * 64) void lz4_exec_kernel(
 }
 
 }  // namespace
+
+#ifdef FSG_STAMPS
+extern "C" int fsg_debug_l4stamps(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_l4_stamps), sizeof(g_l4_stamps));
+  if (reset) {
+    unsigned long long z[8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_l4_stamps), z, sizeof(z));
+  }
+  return e == hipSuccess ? 0 : -1;
+}
+#endif
 
 // Workspace: [0, 256) counters | bm_base[n] | hdr[n] | bitmap words
 // (round_up(ceil(block / 32), 4) per message <= total / 32 + 4 n).
