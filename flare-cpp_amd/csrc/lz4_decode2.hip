@@ -725,7 +725,12 @@ __device__ __forceinline__ void lz4_exec_message(
 
     // ---------- rounds B: the near match chunks in dependency order (as the
     // Snappy pass 2: a chunk runs once its source ends at or below the first
-    // unfinished chunk; read-modify-write merges exactly n bytes)
+    // unfinished chunk; read-modify-write merges exactly n bytes).  C3 text
+    // takes 6.5 rounds per group.  Also letting a chunk run once no other
+    // pending lane's output overlaps its source (the overlapping lanes found
+    // by two binary searches over the lanes' output bounds, ds_bpermute)
+    // cut that only to 5.2 -- the dependencies are real chains -- and was
+    // slower (exec 5.57 -> 6.30 ms, A/B on one box).
     u32 rem = (fits && !is_last && kc < nch) ? ml - 16 * kc : 0u;
     u32 cw = wm + 16 * kc;
     u32 sw = (u32)((int)mo - sbase) + 16 * kc;
@@ -770,6 +775,8 @@ __device__ __forceinline__ void lz4_exec_message(
 #endif
 }
 
+// 7 waves per SIMD (72 VGPRs): exec 5.79 -> 5.49 ms against 6 (A/B, one
+// box); 8 (64 VGPRs, 18 spilled, 2,816-byte window) 7.6 ms.
 #ifndef FSG_L4_EXEC_WAVES
 #define FSG_L4_EXEC_WAVES 7
 #endif
