@@ -52,10 +52,12 @@ constexpr u32 kPredNone = 0xff, kPredUnknown = 0xfe;
 // Diagnostic build only (-DFSG_STAMPS): per-phase cycle totals of the wave
 // encoder, summed over waves (fsg_debug_wstamps).
 #ifdef FSG_STAMPS
-__device__ unsigned long long g_wstamps[8];
+__device__ unsigned long long g_wstamps[12];  // 0-7 cycles per phase, 8-11 counts
 #define STAMP(k) do { const u64 t_ = __builtin_amdgcn_s_memtime(); st_[k] += t_ - t_last_; t_last_ = t_; } while (0)
+#define WCOUNT(k) (st_[k] += 1)
 #else
 #define STAMP(k) do { } while (0)
+#define WCOUNT(k) do { } while (0)
 #endif
 
 __device__ __forceinline__ u32 rl(u32 v, u32 l) { return (u32)__builtin_amdgcn_readlane((int)v, (int)l); }
@@ -141,7 +143,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
                              u16* table, u32 ht, u8* pscr, u8* stg, u32 lane) {
   const int shift = 32 - (31 - __builtin_clz(ht));
 #ifdef FSG_STAMPS
-  u64 st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u64 st_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   u64 t_last_ = __builtin_amdgcn_s_memtime();
 #endif
   // zeroed table (snappy.cc:247-271)
@@ -412,8 +414,11 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       auto scan = [&](u32 k, u64 Ims) -> u32 {
         const u32 hk = rl(h, k), xk = rl(X, k);
         u32 j = 64;
-        for (int i = (int)k - 1; i >= 0; --i)
+        WCOUNT(10);
+        for (int i = (int)k - 1; i >= 0; --i) {
+          WCOUNT(11);
           if (((Ims >> i) & 1ull) && rl(h, (u32)i) == hk) { j = (u32)i; break; }
+        }
         if (j == 64) return rl(packT, k);
         W5 a, b;
 #pragma unroll
@@ -555,6 +560,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
             emit_copy(q - cand, mlen);
           }
         }
+        WCOUNT(9);
         ip = q + mlen;
         next_emit = ip;
         if (ip >= lim) { done = true; break; }
@@ -573,6 +579,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       if (!emit_pending(B, X, xwp.w[0])) return nullptr;
       pend_end = opos;
       STAMP(5);
+      WCOUNT(8);
       if (done) break;
       // the next block's speculation holds only for block B + 64
       const u32 npos = post ? ip : p;
@@ -588,7 +595,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
   STAMP(6);
 #ifdef FSG_STAMPS
   if (lane == 0)
-    for (int k = 0; k < 8; ++k) atomicAdd(&g_wstamps[k], (unsigned long long)st_[k]);
+    for (int k = 0; k < 12; ++k) atomicAdd(&g_wstamps[k], (unsigned long long)st_[k]);
 #endif
   return obase + opos;
 }
@@ -597,7 +604,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
 extern "C" int fsg_debug_wstamps(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), sizeof(g_wstamps));
   if (reset) {
-    unsigned long long z[8] = {};
+    unsigned long long z[12] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wstamps), z, sizeof(z));
   }
   return e == hipSuccess ? 0 : -1;

@@ -28,7 +28,9 @@ def main():
     codec = fsg.SnappyGPU(0)
     lib = codec.lib
     lib.fsg_debug_wstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    b = fsg.make_batch(fsg.KIND_TEXT, np.full(n, size, np.uint32))
+    kind = sys.argv[3] if len(sys.argv) > 3 else "text"  # text | proto (SnappyMessageProto, C5's bodies)
+    b = fsg.make_batch(fsg.KIND_PROTO if kind == "proto" else fsg.KIND_TEXT, np.full(n, size, np.uint32))
+    size = int(b.lens.max())
     dev = torch.device("cuda", 0)
     H = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     caps = np.array([fsg.max_compressed_length(int(x)) for x in b.lens], np.uint64)
@@ -38,7 +40,7 @@ def main():
     d_co, d_cl = H(coff), torch.zeros(n, dtype=torch.int32, device=dev)
     d_st = torch.zeros(n, dtype=torch.int32, device=dev)
     ws = codec.compress_workspace(n, size)
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 12)()
     for _ in range(2):
         lib.fsg_debug_wstamps(buf, 1)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -48,9 +50,11 @@ def main():
         torch.cuda.synchronize()
     lib.fsg_debug_wstamps(buf, 1)
     tot = sum(buf[k] for k in range(8))
-    blocks = n * ((size + 63) // 64)
+    blocks = max(1, buf[8])
     print(f"messages={n} size={size} time={ev0.elapsed_time(ev1):.2f} ms total wave-cycles={tot:.3e} "
           f"per fragment={tot / n:.0f} per block={tot / blocks:.0f}")
+    print(f"  blocks={buf[8]} events/block={buf[9] / blocks:.2f} scans/block={buf[10] / blocks:.3f} "
+          f"scan steps/block={buf[11] / blocks:.2f}")
     for k, name in enumerate(PHASES):
         print(f"  {name:24s} {100.0 * buf[k] / max(tot, 1):5.1f}%  {buf[k] / blocks:8.0f} cyc/block")
 
