@@ -51,11 +51,17 @@ namespace {
 // ---- pass 1 geometry
 constexpr u32 kL4RingChunks = 16;  // per-lane input ring: 16 chunks of 16 bytes
 constexpr u32 kL4RingDwords = 4 * kL4RingChunks;
+#ifndef FSG_L4_TWO_PER_STEP
+#define FSG_L4_TWO_PER_STEP 1
+#endif
 #ifndef FSG_L4_AHEAD
 #define FSG_L4_AHEAD 8
 #endif
+// 12 steps of up to two sequences per iteration: C3 LZ4 index 2.97 ms (24
+// single-sequence steps) -> 2.43 (10: 2.41, 8: 2.45, 16: 2.88, 24: 4.19 --
+// the parse outruns the ring's loads; 12 with 10 chunks ahead: 2.47).
 #ifndef FSG_L4_STEPS
-#define FSG_L4_STEPS 24
+#define FSG_L4_STEPS 12
 #endif
 constexpr u32 kL4Ahead = FSG_L4_AHEAD;  // chunks loaded per iteration
 constexpr int kL4Steps = FSG_L4_STEPS;  // half-steps (token or offset field) per iteration
@@ -276,10 +282,41 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
       st = nst;
       stall = stall || (tstage && !tfail && slow0) || m_stall;
       const bool to_half1 = (t_ok && !last && !fused) || m_stall;
+      const u32 pos0 = pos;
       pos = m_ok ? qpos + 2 + (mx ? 1u : 0u) : (to_half1 ? qpos : pos);
       op = m_ok ? opb + ml : (to_half1 ? opb : op);
       nib = to_half1 ? nv : nib;
       half = m_ok ? false : (to_half1 ? true : half);
+#if FSG_L4_TWO_PER_STEP
+      // ---- the next sequence in the same step, when its token and offset
+      // field lie in the 20 bytes read (offsets <= 15 from the first dword)
+      // and it is a plain one: a literal of <= 14 bytes, no 255 match byte,
+      // not the last sequence, every check passing.  Otherwise the next step
+      // takes it the general way (and reports what failed).  pos < n - 4
+      // here: the sequence before was not the last (q + 8 <= n).
+      {
+        const u32 k2 = s + (pos - pos0);
+        const u32 w2 = alignbyte(mux4(D1, D2, D3, D4, k2 >> 2), mux4(D0, D1, D2, D3, k2 >> 2), k2 & 3);
+        const u32 tok2 = w2 & 0xffu, l2 = tok2 >> 4;
+        const u32 k3 = k2 + 1 + l2;
+        const u32 w3 = alignbyte(mux4(D1, D2, D3, D4, k3 >> 2), mux4(D0, D1, D2, D3, k3 >> 2), k3 & 3);
+        const u32 off2 = w3 & 0xffffu, bb2 = (w3 >> 16) & 0xffu;
+        const u32 nib2 = tok2 & 15;
+        const bool mx2 = nib2 == 15;
+        const u32 ml2 = nib2 + 4 + (mx2 ? bb2 : 0u);
+        const u32 opb2 = op + l2;
+        // (not last: lit + 12 <= ulen - op and lit + 8 <= n - (pos + 1), which
+        // also keep the literal inside the input and the output)
+        const bool ok2 = m_ok & (k3 <= 15) & (l2 < 15) & !(mx2 & (bb2 == 255)) &
+                         (l2 + 12 <= ulen - op) & (l2 + 8 <= n - pos - 1) & (off2 != 0) & (off2 <= opb2) &
+                         (ml2 + 5 <= ulen - opb2);
+        const u32 q2 = pos + 1 + l2;
+        atomicOr(&bmr[((pos >> 5) & (kL4BitWords - 1)) * kWave + lane], ok2 ? 1u << (pos & 31) : 0u);
+        atomicOr(&bmr[((q2 >> 5) & (kL4BitWords - 1)) * kWave + lane], ok2 ? 1u << (q2 & 31) : 0u);
+        pos = ok2 ? q2 + 2 + (mx2 ? 1u : 0u) : pos;
+        op = ok2 ? opb2 + ml2 : op;
+      }
+#endif
     }
     // ---------- stalled lanes: extension runs of 255s, from global memory
     if (stall && st < 0) {
