@@ -52,6 +52,10 @@ constexpr u32 kLz4DistanceMax = 65535;
 constexpr u32 kLz4Limit64K = 65536 + kLz4MfLimit - 1;
 constexpr u32 kLz4MaxInput = 0x7E000000u;  // LZ4_MAX_INPUT_SIZE
 constexpr u32 kLz4TableBytes = 16384;       // either table: 8,192 x u16 or 4,096 x u32
+#ifndef FSG_LZ4_BATCH
+#define FSG_LZ4_BATCH 6
+#endif
+constexpr u32 kLz4Batch = FSG_LZ4_BATCH;    // match-search probes loaded together
 
 LZ4_HD u32 lz4_hash(const u8* p, bool small) {
   if (small) return (ld32(p) * 2654435761u) >> (32 - (kLz4HashLog + 1));
@@ -103,20 +107,58 @@ __host__ __device__ u32 lz4_compress_block(const u8* src, u32 n, u8* dst, u8* ta
     u32 fh = lz4_hash(src + ip, small);
     for (;;) {
       u32 match;
-      // find a match: probe with a step that grows after every 64 misses
+      // find a match: probe with a step that grows after every 64 misses.
+      // kLz4Batch probes at a time: their positions, hashes, table entries and
+      // candidate words are loaded together (one round trip each instead of
+      // one per probe), then the probes run in order exactly as the
+      // reference's loop -- a probe's table read sees the writes of the
+      // earlier probes of the batch, taken from the batch itself -- and the
+      // first match ends the batch (the later probes write nothing).
       {
         u32 fwd = ip, step = 1, nb = 1u << kLz4SkipTrigger;
+        u32 h = fh;
         for (;;) {
-          const u32 h = fh, cur = fwd, mi = get(h);
-          ip = fwd;
-          fwd += step;
-          step = nb++ >> kLz4SkipTrigger;
-          if (fwd > mflimit1) goto last_literals;
-          match = mi;
-          fh = lz4_hash(src + fwd, small);
-          put(h, cur);
-          if (!small && mi + kLz4DistanceMax < cur) continue;  // too far
-          if (ld32(src + match) == ld32(src + ip)) break;
+          u32 cur[kLz4Batch], hs[kLz4Batch], mi[kLz4Batch], cw[kLz4Batch], iw[kLz4Batch];
+          bool ok[kLz4Batch];
+          u32 f = fwd, st = step, b = nb, hh = h;
+#pragma unroll
+          for (u32 k = 0; k < kLz4Batch; ++k) {
+            const bool live = k == 0 || ok[k - 1];  // cur[k] <= mflimit1: its bytes are in the block
+            cur[k] = f;
+            hs[k] = hh;
+            f += st;
+            st = b++ >> kLz4SkipTrigger;
+            ok[k] = live && f <= mflimit1;
+            hh = ok[k] ? lz4_hash(src + f, small) : 0u;
+            iw[k] = live ? ld32(src + cur[k]) : 0u;
+          }
+#pragma unroll
+          for (u32 k = 0; k < kLz4Batch; ++k) mi[k] = get(hs[k]);
+#pragma unroll
+          for (u32 k = 1; k < kLz4Batch; ++k)
+#pragma unroll
+            for (u32 j = 0; j < k; ++j) mi[k] = hs[j] == hs[k] ? cur[j] : mi[k];
+#pragma unroll
+          for (u32 k = 0; k < kLz4Batch; ++k) cw[k] = ok[k] ? ld32(src + mi[k]) : 0u;  // (an invalid probe's
+                                                                                      // position may lie past n)
+          bool found = false;
+#pragma unroll
+          for (u32 k = 0; k < kLz4Batch; ++k) {
+            ip = cur[k];
+            if (!ok[k]) goto last_literals;
+            match = mi[k];
+            put(hs[k], cur[k]);
+            if (!small && mi[k] + kLz4DistanceMax < cur[k]) continue;  // too far
+            if (cw[k] == iw[k]) {
+              found = true;
+              break;
+            }
+          }
+          if (found) break;
+          fwd = f;
+          step = st;
+          nb = b;
+          h = hh;
         }
       }
       while (ip > anchor && match > 0 && src[ip - 1] == src[match - 1]) {  // extend backwards
