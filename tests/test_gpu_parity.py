@@ -718,6 +718,34 @@ def test_wave_encoder_against_oracle(gpu, oracle, wave_min, all_mb, monkeypatch)
         assert all(c == oracle.compress(x) for x, c in zip(big, comps))
 
 
+def test_small_batch_wave_encoder(gpu, oracle):
+    """Batches of <= 64 messages put every message of >= 15 bytes on the wave
+    encoder (snappy_encode_v3.hip kSmallBatchEnc).  Batches of 1, 7 and 64
+    messages over golden inputs, random alphabets, periodic data, long runs,
+    split messages and the input-margin edge sizes: bytes equal the
+    oracle's."""
+    vecs = json.loads((GOLDEN / "vectors.json").read_text())
+    items = [build_input(v) for v in vecs]
+    rng = np.random.default_rng(77)
+    for n in (14, 15, 16, 17, 31, 63, 64, 65, 127, 4095, 4096, 65535, 65536, 65537):
+        items.append(fsg.make_batch(fsg.KIND_TEXT, [n], first_index=n).item(0))
+    for t in range(60):
+        n = int(rng.choice([rng.integers(0, 5000), rng.integers(0, 140000)]))
+        alpha = int(rng.choice([2, 3, 8, 40, 256]))
+        items.append(rng.integers(0, alpha, n, dtype=np.uint8).tobytes())
+    for per in (1, 3, 17, 61):
+        items.append(bytes(((np.arange(30000 + per) % per) * 7 + 1).astype(np.uint8)))
+    items.append(bytes(70000))
+    items.append(fsg.make_batch(fsg.KIND_TEXT, [200000], first_index=5).item(0))
+    for size in (1, 7, 64):
+        for b0 in range(0, len(items), size if size > 1 else 9):
+            part = items[b0:b0 + size]
+            comps, st = gpu.compress(fsg.Batch.from_list(part))
+            assert (st == 0).all()
+            for i, (x, c) in enumerate(zip(part, comps)):
+                assert c == oracle.compress(x), (size, b0 + i, len(x))
+
+
 @pytest.mark.parametrize("name", ["C3", "C5"])
 def test_wave_encoder_config_digests(gpu, name, monkeypatch):
     """Config digests (reference-generated) with the wave encoder on every
