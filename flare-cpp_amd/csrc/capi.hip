@@ -48,7 +48,7 @@ hipError_t launch_lz4_decode(const u8* in, const u64* in_off, const u32* in_len,
 size_t lz4_decode_workspace_bytes(u32 n_msgs, u64 total_in_bytes);
 hipError_t launch_lz4_decode2(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u8* out,
                               const u64* out_off, const u32* out_cap, u32* out_len, i32* status, void* ws,
-                              size_t ws_bytes, hipStream_t stream);
+                              size_t ws_bytes, hipStream_t stream, hipStream_t pass1_stream);
 }  // namespace fsg
 
 namespace {
@@ -319,8 +319,33 @@ int fsg_lz4_decompress_batch_ws(const uint8_t* d_in, const uint64_t* d_in_off, c
     return fsg_lz4_decompress_batch(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
                                     d_status, stream);
   return record(fsg::launch_lz4_decode2(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
-                                        d_status, d_workspace, workspace_bytes, (hipStream_t)stream),
+                                        d_status, d_workspace, workspace_bytes, (hipStream_t)stream, nullptr),
                 "fsg_lz4_decompress_batch_ws");
+}
+
+int fsg_lz4_decompress_batch_2s(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                                uint32_t n_msgs, uint8_t* d_out, const uint64_t* d_out_off,
+                                const uint32_t* d_out_cap, uint32_t* d_out_len, int32_t* d_status,
+                                void* d_workspace, size_t workspace_bytes, void* stream, void* pass1_stream) {
+  if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_cap || !d_out_len || !d_status))
+    return FSG_ERR_INVALID_ARG;
+  if (!d_workspace || workspace_bytes < fsg::lz4_decode_workspace_bytes(n_msgs, 0)) {
+    // the one-pass kernel on `stream`, ordered behind pass1_stream's work
+    if (pass1_stream && pass1_stream != stream) {
+      hipEvent_t ev = nullptr;
+      hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      if (e == hipSuccess) e = hipEventRecord(ev, (hipStream_t)pass1_stream);
+      if (e == hipSuccess) e = hipStreamWaitEvent((hipStream_t)stream, ev, 0);
+      if (ev) (void)hipEventDestroy(ev);
+      if (e != hipSuccess) return record(e, "fsg_lz4_decompress_batch_2s");
+    }
+    return fsg_lz4_decompress_batch(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                    d_status, stream);
+  }
+  return record(fsg::launch_lz4_decode2(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_out_len,
+                                        d_status, d_workspace, workspace_bytes, (hipStream_t)stream,
+                                        (hipStream_t)pass1_stream),
+                "fsg_lz4_decompress_batch_2s");
 }
 
 }  // extern "C"

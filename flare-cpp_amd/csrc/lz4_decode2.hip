@@ -38,6 +38,8 @@
 //
 // Messages whose bitmap does not fit the workspace get kNeedFallback and are
 // decoded by lz4.hip's lane-per-message kernel.
+#include <mutex>
+
 #include "wave_util.h"
 
 namespace fsg {
@@ -856,24 +858,64 @@ size_t lz4_decode_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
   return kL4Head + 2 * l4_list_bytes(n_msgs) + 4 * (total_in_bytes / 32 + 4 * (u64)n_msgs + 4);
 }
 
+// Per-device event that orders the execution pass behind the index pass in
+// the two-stream form (created on first use; nullptr: one stream).
+namespace {
+struct L4Two {
+  hipEvent_t pass1 = nullptr;
+  std::mutex mu;
+};
+L4Two* l4_two() {
+  constexpr int kMaxDevices = 64;
+  static L4Two g[kMaxDevices];
+  static std::once_flag once[kMaxDevices];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+  L4Two* t = &g[dev];
+  std::call_once(once[dev], [t] {
+    if (hipEventCreateWithFlags(&t->pass1, hipEventDisableTiming) != hipSuccess) t->pass1 = nullptr;
+  });
+  return t->pass1 ? t : nullptr;
+}
+}  // namespace
+
 hipError_t launch_lz4_decode2(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u8* out,
                               const u64* out_off, const u32* out_cap, u32* out_len, i32* status, void* ws,
-                              size_t ws_bytes, hipStream_t stream) {
+                              size_t ws_bytes, hipStream_t stream, hipStream_t pass1_stream) {
   if (n_msgs == 0) return hipSuccess;
   const u64 fixed = kL4Head + 2 * l4_list_bytes(n_msgs);
   if (ws_bytes < fixed) return hipErrorInvalidValue;
+  // Two-stream form (as launch_decode_v4's): the index pass on pass1_stream,
+  // the execution and fallback passes on `stream` behind an event, so a
+  // caller's next batch walks while this one executes
+  L4Two* two = pass1_stream && pass1_stream != stream ? l4_two() : nullptr;
+  hipStream_t s1 = two ? pass1_stream : stream;
+  hipError_t e = hipSuccess;
+  if (pass1_stream && pass1_stream != stream && !two) {  // no event: order stream behind pass1_stream
+    hipEvent_t ev = nullptr;
+    e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev, pass1_stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev, 0);
+    if (ev) (void)hipEventDestroy(ev);
+    if (e != hipSuccess) return e;
+  }
   u8* w = static_cast<u8*>(ws);
   u32* counter = reinterpret_cast<u32*>(w);
   u32* bm_base = reinterpret_cast<u32*>(w + kL4Head);
   u32* hdr = reinterpret_cast<u32*>(w + kL4Head + l4_list_bytes(n_msgs));
   u32* bitmap = reinterpret_cast<u32*>(w + fixed);
   const u64 cap_words = (ws_bytes - fixed) / 16 * 4;  // whole 16-byte groups
-  hipError_t e = hipMemsetAsync(counter, 0, kL4Head, stream);
+  e = hipMemsetAsync(counter, 0, kL4Head, s1);
   if (e != hipSuccess) return e;
-  lz4_index_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out_cap, out_len, status,
-                                                         counter, bm_base, hdr, bitmap, cap_words);
+  lz4_index_kernel<<<(n_msgs + 63) / 64, 64, 0, s1>>>(in, in_off, in_len, n_msgs, out_cap, out_len, status,
+                                                      counter, bm_base, hdr, bitmap, cap_words);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (two) {
+    std::lock_guard<std::mutex> lk(two->mu);
+    if ((e = hipEventRecord(two->pass1, s1)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(stream, two->pass1, 0)) != hipSuccess) return e;
+  }
   lz4_exec_kernel<<<(n_msgs + kL4Waves - 1) / kL4Waves, kL4Waves * 64, 0, stream>>>(
       in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, hdr, bitmap);
   e = hipGetLastError();

@@ -46,6 +46,8 @@ _SIGS = {
     "fsg_lz4_decompress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "fsg_lz4_decompress_workspace_bytes": (_sz, [_u32, _u64]),
     "fsg_lz4_decompress_batch_ws": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    "fsg_lz4_decompress_batch_2s": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp,
+                                               _vp]),
 }
 
 
@@ -58,7 +60,7 @@ def header_symbols(header: Path | None = None) -> list[str]:
 
 
 # entry points an older library under A/B may lack
-_OPTIONAL = {"fsg_decompress_batch_2s"}
+_OPTIONAL = {"fsg_decompress_batch_2s", "fsg_lz4_decompress_batch_2s"}
 
 
 def load_gpu_lib(path: Path | None = None) -> ctypes.CDLL:
@@ -158,18 +160,23 @@ class SnappyGPU:
         return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device or f"cuda:{self.device}")
 
     def lz4_decompress(self, d_in, d_in_off, d_in_len, n, d_out, d_out_off, d_out_cap, d_out_len, d_status,
-                       stream=None, workspace=None):
+                       stream=None, workspace=None, pass1_stream=None):
         """workspace=None: the one-pass lane kernel; else the two-pass
-        decoder (fsg_lz4_decompress_batch_ws)."""
+        decoder (fsg_lz4_decompress_batch_ws; with `pass1_stream`,
+        fsg_lz4_decompress_batch_2s: the index pass there, the execution on
+        `stream`)."""
         if workspace is None:
             self._check(self.lib.fsg_lz4_decompress_batch(
                 _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off), _ptr(d_out_cap),
                 _ptr(d_out_len), _ptr(d_status), self._stream(stream)), "fsg_lz4_decompress_batch")
             return
-        self._check(self.lib.fsg_lz4_decompress_batch_ws(
-            _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off), _ptr(d_out_cap),
-            _ptr(d_out_len), _ptr(d_status), _ptr(workspace), workspace.numel(), self._stream(stream)),
-            "fsg_lz4_decompress_batch_ws")
+        args = (_ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off), _ptr(d_out_cap),
+                _ptr(d_out_len), _ptr(d_status), _ptr(workspace), workspace.numel(), self._stream(stream))
+        if pass1_stream is None:
+            self._check(self.lib.fsg_lz4_decompress_batch_ws(*args), "fsg_lz4_decompress_batch_ws")
+        else:
+            self._check(self.lib.fsg_lz4_decompress_batch_2s(*args, self._stream(pass1_stream)),
+                        "fsg_lz4_decompress_batch_2s")
 
     def uncompressed_lengths(self, d_in, d_in_off, d_in_len, n, d_ulen, lenient=True, stream=None):
         self._check(self.lib.fsg_uncompressed_lengths_batch(

@@ -73,6 +73,23 @@ int fsg_lz4_decompress_batch_ws(const uint8_t *d_in, const uint64_t *d_in_off,
                                 int32_t *d_status, void *d_workspace,
                                 size_t workspace_bytes, void *stream);
 
+/* fsg_lz4_decompress_batch_ws in two streams: the index pass (validation +
+ * sequence bitmap) on `pass1_stream`, the execution and fallback passes on
+ * `stream` behind an event, so that batch k+1's index pass (latency-bound,
+ * one lane per message) runs beside batch k's execution (issue-bound) when
+ * the two batches have their own workspace, output, d_out_len and d_status
+ * buffers.  The inputs must be ready on `pass1_stream`; calls sharing any of
+ * those buffers must be ordered by the caller.  Results are valid once
+ * `stream` is synchronised.  Same statuses and bytes as
+ * fsg_lz4_decompress_batch.  (Snappy's counterpart: fsg_decompress_batch_2s.) */
+int fsg_lz4_decompress_batch_2s(const uint8_t *d_in, const uint64_t *d_in_off,
+                                const uint32_t *d_in_len, uint32_t n_msgs,
+                                uint8_t *d_out, const uint64_t *d_out_off,
+                                const uint32_t *d_out_cap, uint32_t *d_out_len,
+                                int32_t *d_status, void *d_workspace,
+                                size_t workspace_bytes, void *stream,
+                                void *pass1_stream);
+
 #ifdef __cplusplus
 }
 #endif

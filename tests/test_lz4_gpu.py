@@ -194,3 +194,57 @@ def test_lz4_two_pass_c3_like_batch(gpu, o):
     bodies = [o.compress(x) for x in xs]
     outs, ol, st = gpu.lz4_decompress(bodies, [len(x) for x in xs])
     assert (st == 0).all() and all(y == x for y, x in zip(outs, xs))
+
+
+def test_lz4_two_stream_form(gpu, o):
+    """fsg_lz4_decompress_batch_2s: two batches with their own buffers,
+    decoded alternately four times, each batch's index pass on a second
+    stream beside the other's execution (the slot's previous execution
+    waited for by event, as bench.py's time_pipelined does): the verdicts and
+    bytes of the oracle every time, a corrupt body and a slot too small among
+    them."""
+    import torch
+    from gpu_harness import POISON
+    rng = np.random.default_rng(57)
+    dev = torch.device("cuda", 0)
+    H = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    slots = []
+    for t in range(2):
+        xs = _kinds(rng, 30)
+        bodies = [o.compress(x) for x in xs]
+        bodies[5] = bodies[5][:-1] if len(bodies[5]) > 2 else bodies[5]
+        caps = [len(x) for x in xs]
+        caps[7] = max(caps[7] - 1, 0)
+        ref = [o.uncompress(b, cap=c) for b, c in zip(bodies, caps)]
+        b = fsg.Batch.from_list(bodies)
+        n = len(b)
+        capa = np.array(caps, dtype=np.uint32)
+        oo, tot = fsg.slot_offsets(capa.astype(np.uint64))
+        slots.append(dict(n=n, ref=ref, oo=oo, caps=capa, d_in=H(b.data), d_io=H(b.offsets), d_il=H(b.lens),
+                          d_oo=H(oo), d_cap=H(capa),
+                          d_out=torch.full((max(tot, 1),), POISON, dtype=torch.uint8, device=dev),
+                          d_ol=torch.zeros(n, dtype=torch.int32, device=dev),
+                          d_st=torch.full((n,), -7, dtype=torch.int32, device=dev),
+                          ws=gpu.codec.lz4_decompress_workspace(n, int(b.data.size))))
+    s = torch.cuda.current_stream(dev)
+    s1 = torch.cuda.Stream(dev)
+    done = [None, None]
+    for k in range(8):
+        sl = slots[k % 2]
+        if done[k % 2] is not None:
+            s1.wait_event(done[k % 2])
+        gpu.codec.lz4_decompress(sl["d_in"], sl["d_io"], sl["d_il"], sl["n"], sl["d_out"], sl["d_oo"], sl["d_cap"],
+                                 sl["d_ol"], sl["d_st"], stream=s, workspace=sl["ws"], pass1_stream=s1)
+        ev = torch.cuda.Event()
+        ev.record(s)
+        done[k % 2] = ev
+    torch.cuda.synchronize()
+    code = {1: 0, 0: fsg.FSG_CORRUPT, -1: fsg.FSG_BAD_HEADER, -2: fsg.FSG_SLOT_TOO_SMALL}
+    for sl in slots:
+        st = sl["d_st"].cpu().numpy()
+        out = sl["d_out"].cpu().numpy()
+        for i, (r, _, y0) in enumerate(sl["ref"]):
+            assert st[i] == code[r], i
+            if r == 1:
+                a = int(sl["oo"][i])
+                assert out[a:a + len(y0)].tobytes() == y0, i

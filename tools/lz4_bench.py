@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--two-pass-only", action="store_true", help="skip the one-pass decode timing")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU lines")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="skip the stream of two alternating batches (fsg_lz4_decompress_batch_2s)")
     a = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
@@ -83,6 +85,40 @@ def main():
     d_out.fill_(0xA5)
     dec2_ms = timed(dec2)
     dec2_ok = int((d_st != 0).sum().item()) == 0 and bool(torch.equal(d_out, d_raw))
+    # A stream of two alternating batches (the second one distinct), batch
+    # k+1's index pass on a second stream beside batch k's execution
+    # (fsg_lz4_decompress_batch_2s; bench.py's time_pipelined)
+    pipe = None
+    if not a.no_pipelined:
+        sys.path.insert(0, str(REPO))
+        from bench import time_pipelined
+        batch2 = fsg.make_batch(fsg.KIND_TEXT, np.full(a.n, a.size, np.uint32), first_index=a.n)
+        d_raw2, d_ro2, d_rl2 = H(batch2.data), H(batch2.offsets), H(batch2.lens)
+        d_c2 = torch.zeros(c_tot, dtype=torch.uint8, device=dev)
+        d_cl2 = torch.zeros(n, dtype=torch.int32, device=dev)
+        d_st2 = torch.zeros(n, dtype=torch.int32, device=dev)
+        codec.lz4_compress(d_raw2, d_ro2, d_rl2, n, d_c2, d_co, d_cl2, d_st2, ws, stream=s)
+        d_out2 = torch.full((raw,), 0xA5, dtype=torch.uint8, device=dev)
+        d_ol2 = torch.zeros(n, dtype=torch.int32, device=dev)
+        dws2 = codec.lz4_decompress_workspace(n, int(c_tot))
+        d_out.fill_(0xA5)
+        slots = [(d_c, d_cl, d_out, d_ro, d_rl, d_ol, d_st, dws), (d_c2, d_cl2, d_out2, d_ro2, d_rl2, d_ol2, d_st2, dws2)]
+
+        def issue(k, s1):
+            c, cl, o, ro, rl, ol, st, w = slots[k % 2]
+            codec.lz4_decompress(c, d_co, cl, n, o, ro, rl, ol, st, stream=s, workspace=w, pass1_stream=s1)
+
+        steps = max(2, a.steps - a.steps % 2)
+        _, t_ev, lat = time_pipelined(torch, dev, s, slots, issue, steps, 2, 1, None)
+        ok = (int((d_st != 0).sum().item()) == 0 and int((d_st2 != 0).sum().item()) == 0
+              and bool(torch.equal(d_out, d_raw)) and bool(torch.equal(d_out2, d_raw2)))
+        raw2 = (raw + int(batch2.total)) / 2
+        pipe = {"ms": round(t_ev * 1e3, 3), "gib_s": round(raw2 / t_ev / GIB, 3), "roundtrip_ok": ok,
+                "latency_ms": round(lat * 1e3, 3), "steps": steps,
+                "roofline_frac": round((raw2 + comp) / t_ev / 8e12, 4),
+                "mode": "two alternating batches; batch k+1's index pass on a second stream beside batch k's "
+                        "execution (fsg_lz4_decompress_batch_2s)"}
+        del d_raw2, d_c2, d_out2, dws2
     from bind import Lz4Oracle
     o = Lz4Oracle()
     host_c = d_c.cpu().numpy()
@@ -128,6 +164,7 @@ def main():
                    "roofline_frac": round((raw + comp) / (dec_ms / 1e3) / 8e12, 4)},
         "decode_two_pass": {"ms": round(dec2_ms, 3), "gib_s": round(raw / (dec2_ms / 1e3) / GIB, 3),
                             "roundtrip_ok": dec2_ok, "roofline_frac": round((raw + comp) / (dec2_ms / 1e3) / 8e12, 4)},
+        "decode_two_pass_pipelined": pipe,
         "oracle_sample_ok": sample_ok,
         "cpu_oracle_1thread": {"compress_gib_s": round(kb / t_oc / GIB, 3), "decompress_gib_s": round(kb / t_od / GIB, 3),
                                "sample": f"first {k} bodies"},

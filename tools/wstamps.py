@@ -9,7 +9,9 @@ import sys
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
-os.environ["FSG_LIB"] = str(REPO / "flare-cpp_amd" / "lib" / "libflare_snappy_gpu_stamps.so")
+STAMPS = not os.environ.get("FSG_NOSTAMPS")  # FSG_NOSTAMPS=1: the default library, timing only (for --pmc runs)
+if STAMPS:
+    os.environ["FSG_LIB"] = str(REPO / "flare-cpp_amd" / "lib" / "libflare_snappy_gpu_stamps.so")
 os.environ["FSG_ENCODE_WAVE_MIN"] = os.environ.get("FSG_ENCODE_WAVE_MIN", "1")
 os.environ["FSG_ENCODE_WAVE_ALL_MB"] = os.environ.get("FSG_ENCODE_WAVE_ALL_MB", "100000")  # every unit on the wave encoder
 sys.path.insert(0, str(REPO / "flare-cpp_amd" / "py"))
@@ -27,7 +29,8 @@ def main():
     size = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
     codec = fsg.SnappyGPU(0)
     lib = codec.lib
-    lib.fsg_debug_wstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    if STAMPS:
+        lib.fsg_debug_wstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     kind = sys.argv[3] if len(sys.argv) > 3 else "text"  # text | proto (SnappyMessageProto, C5's bodies)
     b = fsg.make_batch(fsg.KIND_PROTO if kind == "proto" else fsg.KIND_TEXT, np.full(n, size, np.uint32))
     size = int(b.lens.max())
@@ -42,12 +45,16 @@ def main():
     ws = codec.compress_workspace(n, size)
     buf = (ctypes.c_ulonglong * 12)()
     for _ in range(2):
-        lib.fsg_debug_wstamps(buf, 1)
+        if STAMPS:
+            lib.fsg_debug_wstamps(buf, 1)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
         codec.compress(d_raw, d_ro, d_rl, n, size, d_c, d_co, d_cl, d_st, workspace=ws)
         ev1.record()
         torch.cuda.synchronize()
+    if not STAMPS:
+        print(f"messages={n} size={size} time={ev0.elapsed_time(ev1):.2f} ms")
+        return
     lib.fsg_debug_wstamps(buf, 1)
     tot = sum(buf[k] for k in range(8))
     blocks = max(1, buf[8])
