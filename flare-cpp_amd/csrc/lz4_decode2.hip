@@ -38,6 +38,7 @@
 //
 // Messages whose bitmap does not fit the workspace get kNeedFallback and are
 // decoded by lz4.hip's lane-per-message kernel.
+#include <cstdlib>
 #include <mutex>
 
 #include "wave_util.h"
@@ -148,7 +149,7 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u32 n_msgs,
     const u32* __restrict__ out_cap, u32* __restrict__ out_len, i32* __restrict__ status_out,
     u32* __restrict__ bm_counter, u32* __restrict__ bm_base_out, u32* __restrict__ hdr_out,
-    u32* __restrict__ bitmap, u64 bm_capacity_words) {
+    u32* __restrict__ bitmap, u64 bm_capacity_words, u32* __restrict__ big_list, u32 big_min) {
   // [dword][lane]; rows kL4RingDwords.. +3 repeat rows 0..3 (a 5-dword read
   // at the ring's end wraps)
   __shared__ u32 ring[(kL4RingDwords + 4) * kWave];
@@ -187,6 +188,12 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
   if (valid) {
     bm_base_out[m] = bmb;
     hdr_out[m] = h;
+  }
+  // blocks of more than big_min bytes: walked by lz4_index_big_kernel, a wave
+  // per message (a lane takes ~60 ms per MB; bm_counter[1] counts the list)
+  if (st < 0 && n > big_min) {
+    st = kNeedBigIndex;
+    big_list[atomicAdd(&bm_counter[1], 1u)] = m;
   }
   u32* bm = bitmap + bmb;
 
@@ -413,6 +420,289 @@ __global__ __launch_bounds__(64) void lz4_index_kernel(
 #undef L4_CHUNK
 #undef L4_RING_WRITE
   if (valid) status_out[m] = st;
+}
+
+// ===========================================================================
+// Pass 1, large blocks: one WAVE per listed message.  The lane walk reads its
+// input through a 256-byte per-lane ring loaded 128 bytes per iteration, and a
+// lone lane takes ~60 ms per MB.  Here the wave stages the block into an 8 KiB
+// LDS ring, 4 KiB (64 lanes x 64 bytes) at a time, and indexes it 64 bytes
+// per step, as the Snappy pass 1b (snappy_decode_v4.hip, index_big_message):
+// every lane decodes the sequence that would start at its byte (literal
+// length, offset field, match length, successor, the checks that need no walk
+// state), the real sequence starts in the window -- the chain from the
+// current position -- come from pointer doubling over the successors, their
+// output positions from a prefix sum, and the position-dependent checks of
+// lz4o_decompress_block run on all of them at once.  A sequence the window
+// cannot decode (a 255 extension byte, an offset field more than 20 bytes on)
+// is taken by a wave-uniform serial step.  Bits: the block's bitmap words are
+// zeroed first, then ORed in.
+constexpr u32 kBigRing = 8192;
+constexpr u32 kBigRingDw = kBigRing / 4;
+constexpr u32 kBigHalf = kBigRing / 2;
+constexpr u32 kBigWaves = 4;
+
+__device__ __forceinline__ u32 rfl(u32 v) { return (u32)__builtin_amdgcn_readfirstlane((int)v); }
+
+// 4 bytes at byte k (0..20) of the 24 bytes X01 | X23 << 64 | X45 << 128
+__device__ __forceinline__ u32 window4(u64 X01, u64 X23, u64 X45, u32 k) {
+  const u64 lo = k < 8 ? X01 : (k < 16 ? X23 : X45);
+  const u64 hi = k < 8 ? X23 : X45;
+  const u32 sh = 8 * (k & 7);
+  return sh ? (u32)((lo >> sh) | (hi << (64 - sh))) : (u32)lo;
+}
+
+__device__ i32 lz4_walk_big(u32 m, const u8* __restrict__ in, const u64* __restrict__ in_off,
+                            const u32* __restrict__ in_len, const u32* __restrict__ out_len,
+                            const u32* __restrict__ bm_base, const u32* __restrict__ hdr, u32* __restrict__ bitmap,
+                            u32* ring, u32 lane) {
+  const u32 h = rfl(hdr[m]);
+  const u32 ulen = rfl(out_len[m]);
+  const u32 n = rfl(in_len[m]) - h;  // > big_min > 0
+  const u8* bb = in + in_off[m] + h;
+  u32* bm = bitmap + rfl(bm_base[m]);
+  const u32 words = (((n + 31) >> 5) + 3) & ~3u;
+  for (u32 z = 4 * lane; z < words; z += 256) *reinterpret_cast<u32x4*>(bm + z) = u32x4{0, 0, 0, 0};
+  wait_all_memory();  // the zeros land before the ORs
+  const u32 bal = (u32)(reinterpret_cast<uintptr_t>(bb) & 15);
+  const u8* abase = bb - bal;
+  const u32 last_chunk = (bal + n - 1) >> 4;
+  const __amdgpu_buffer_rsrc_t rs = msg_rsrc(abase, bal + n);
+  // 4 bytes at block position p from global memory (bytes past the block read 0)
+  auto g4 = [&](u32 p) -> u32 {
+    const u32 P = p + bal;
+    const u32 lo = rfl(__builtin_amdgcn_raw_buffer_load_b32(rs, P & ~3u, 0, 0));
+    const u32 hi = rfl(__builtin_amdgcn_raw_buffer_load_b32(rs, (P & ~3u) + 4, 0, 0));
+    return (u32)((((u64)hi << 32) | lo) >> (8 * (P & 3)));
+  };
+  // ring slots of chunks [c0, c0 + nch) (16-byte chunks from abase)
+  auto stage = [&](u32 c0, u32 nch) {
+    wave_lds_fence();
+    for (u32 r = 0; r < nch; r += 64) {
+      const u32 k = c0 + r + lane;
+      const u32 kk = k <= last_chunk ? k : last_chunk;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(abase + 16 * kk);
+      *reinterpret_cast<u32x4*>(ring + ((4 * k) & (kBigRingDw - 1))) = v;
+    }
+    wave_lds_fence();
+    if (lane < 8) ring[kBigRingDw + lane] = ring[lane];  // reads that wrap the ring's end
+    wave_lds_fence();
+  };
+  u32 sb = 0;  // the ring holds input offsets [sb, sb + kBigRing) from abase
+  stage(0, kBigRing / 16);
+  // the ring holds [P, P + 88) after this (P < sb + kBigHalf)
+  auto keep = [&](u32 P) {
+    if (P >= sb + kBigHalf) {  // slide by a half, or restage after a jump
+      const u32 nsb = P & ~(kBigHalf - 1);
+      if (nsb == sb + kBigHalf)
+        stage((sb + kBigRing) >> 4, kBigHalf / 16);
+      else
+        stage(nsb >> 4, kBigRing / 16);
+      sb = nsb;
+    }
+  };
+  // 24 bytes at input offset P from the ring
+  auto read24 = [&](u32 P, u64& X01, u64& X23, u64& X45) {
+    const u32 dw = (P >> 2) & (kBigRingDw - 1), s = 8 * (P & 3);
+    u32 d[7];
+#pragma unroll
+    for (u32 i = 0; i < 7; ++i) d[i] = ring[dw + i];
+    u32 x[6];
+#pragma unroll
+    for (u32 i = 0; i < 6; ++i) x[i] = (u32)((((u64)d[i + 1] << 32) | d[i]) >> s);
+    X01 = ((u64)x[1] << 32) | x[0];
+    X23 = ((u64)x[3] << 32) | x[2];
+    X45 = ((u64)x[5] << 32) | x[4];
+  };
+  auto set_bit = [&](u32 p) {
+    if (lane == 0) __hip_atomic_fetch_or(bm + (p >> 5), 1u << (p & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+
+  u32 pos = 0, op = 0;
+  i32 status = -1;
+  // One sequence at pos, wave-uniform (the lane walk's rules in order,
+  // lz4o_decompress_block :168-202): returns with pos / op advanced, or
+  // status set.
+  auto serial = [&]() {
+    keep(pos + bal);
+    u64 X01, X23, X45;
+    read24(pos + bal, X01, X23, X45);
+    const u32 x0 = rfl((u32)X01);
+    const u32 tok = x0 & 0xffu;
+    u32 lit = tok >> 4, ip = pos + 1;
+    if (lit == 15) {
+      if (ip >= n) {
+        status = kCorrupt;
+        return;
+      }
+      u32 b = (x0 >> 8) & 0xffu;
+      lit += b;
+      ++ip;
+      while (b == 255 && lit <= n) {
+        if (ip >= n) {
+          status = kCorrupt;
+          return;
+        }
+        b = g4(ip) & 0xffu;
+        ++ip;
+        lit += b;
+      }
+    }
+    if (lit > n - ip || lit > ulen - op) {
+      status = kCorrupt;
+      return;
+    }
+    set_bit(pos);
+    if ((u64)op + lit + 12 > ulen || (u64)ip + lit + 8 > n) {  // the last sequence
+      status = (ip + lit == n && op + lit == ulen) ? kOk : kCorrupt;
+      return;
+    }
+    const u32 q = ip + lit;  // q + 8 <= n
+    op += lit;
+    const u32 k = q - pos;
+    const u32 w = k <= 20 ? rfl(window4(X01, X23, X45, k)) : g4(q);
+    const u32 off = w & 0xffffu;
+    if (off == 0 || off > op) {
+      status = kCorrupt;
+      return;
+    }
+    set_bit(q);
+    const u32 nib = tok & 15;
+    u32 ml = nib + 4;
+    ip = q + 2;
+    if (nib == 15) {
+      u32 b = (w >> 16) & 0xffu;
+      ml += b;
+      ++ip;
+      while (b == 255 && ml <= ulen) {
+        if (ip >= n) {
+          status = kCorrupt;
+          return;
+        }
+        b = g4(ip) & 0xffu;
+        ++ip;
+        ml += b;
+      }
+    }
+    if ((u64)ml + 5 > ulen - op) {
+      status = kCorrupt;
+      return;
+    }
+    op += ml;
+    pos = ip;
+  };
+
+  while (status < 0) {
+    pos = rfl(pos);
+    op = rfl(op);
+    sb = rfl(sb);
+    if (pos >= n) {
+      status = kCorrupt;
+      break;
+    }
+    const u32 wb = pos & ~31u;
+    keep(wb + bal);
+    // ---------- every lane decodes the sequence that would start at p
+    const u32 p = wb + lane;
+    u64 X01, X23, X45;
+    read24(p + bal, X01, X23, X45);
+    const u32 x0 = (u32)X01;
+    const u32 tok = x0 & 0xffu, l0 = tok >> 4, b1 = (x0 >> 8) & 0xffu;
+    const bool lx = l0 == 15;
+    const bool slow_t = lx && b1 == 255;  // a run of 255s: the serial step
+    const u32 lit = l0 + (lx ? b1 : 0u);
+    const u32 ipl = p + 1 + (lx ? 1u : 0u);
+    const bool bad_tok = (p >= n) | (lx & (p + 1 >= n));
+    // (ipl <= n unless bad_tok; u32 differences only read when !bad_tok)
+    const bool bad_lit = !slow_t && lit > n - ipl;
+    const bool last_static = !slow_t && lit + 8 > n - ipl;
+    const u32 k = 1 + (lx ? 1u : 0u) + lit;  // offset field - p
+    const u32 w = window4(X01, X23, X45, k <= 20 ? k : 0u);
+    const u32 off = w & 0xffffu, nib = tok & 15, b2 = (w >> 16) & 0xffu;
+    const bool mx = nib == 15;
+    const u32 ml = nib + 4 + (mx ? b2 : 0u);
+    const bool complex = slow_t || (!last_static && (k > 20 || (mx && b2 == 255)));
+    const u32 succ = p + k + 2 + (mx ? 1u : 0u);
+    const bool stop = bad_tok || bad_lit || last_static || complex || succ >= wb + 64;
+    // ---------- the chain from pos by pointer doubling (J: successor lane,
+    // 64 = none in this window; M: the lanes within 2^r steps).  A sequence
+    // is >= 3 bytes, so <= 22 start in 64 bytes: 5 rounds.
+    u32 J = stop ? 64u : succ - wb;
+    u64 M = 1ull << lane;
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const u32 src = J < 64 ? J : lane;
+      const u64 Mj = ((u64)(u32)__shfl((int)(u32)(M >> 32), (int)src, 64) << 32) |
+                     (u32)__shfl((int)(u32)M, (int)src, 64);
+      const u32 Jj = (u32)__shfl((int)J, (int)src, 64);
+      if (J < 64) {
+        M |= Mj;
+        J = Jj;
+      }
+    }
+    const u32 first = pos - wb;
+    const u64 S = ((u64)readlane((u32)(M >> 32), first) << 32) | readlane((u32)M, first);
+    const bool in_s = (S >> lane) & 1ull;
+    // ---------- output positions and the position-dependent checks
+    // (a chain lane that is not an event below has its lit + ml exact)
+    const u32 len = in_s && !(bad_tok || bad_lit || last_static || complex) ? lit + ml : 0u;
+    const u32 incl = dpp_incl_scan(len);
+    const u32 opk = op + incl - len;
+    const bool e_bad = in_s && (bad_tok || bad_lit || (!slow_t && lit > ulen - opk));
+    const bool e_last = in_s && !e_bad && !slow_t && (last_static || (u64)opk + lit + 12 > ulen);
+    const bool e_cx = in_s && !e_bad && !e_last && complex;
+    const bool e_mbad = in_s && !e_bad && !e_last && !complex &&
+                        (off == 0 || off > opk + lit || (u64)ml + 5 > ulen - opk - lit);
+    const u64 Ev = __ballot(e_bad || e_last || e_cx || e_mbad);
+    const u32 E = Ev ? (u32)__builtin_ctzll(Ev) : 64u;
+    // bits: the chain below the event (and the token of a last sequence)
+    if (in_s && (lane < E || (lane == E && e_last)))
+      __hip_atomic_fetch_or(bm + (p >> 5), 1u << (p & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (in_s && lane < E) {
+      const u32 q = p + k;
+      __hip_atomic_fetch_or(bm + (q >> 5), 1u << (q & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (E < 64) {
+      const u32 kind = readlane(e_bad || e_mbad ? 1u : (e_last ? ((ipl + lit == n && opk + lit == ulen) ? 2u : 1u) : 3u),
+                                E);
+      if (kind == 1) {
+        status = kCorrupt;
+        break;
+      }
+      if (kind == 2) {
+        status = kOk;
+        break;
+      }
+      pos = wb + E;  // a sequence for the serial step
+      op = readlane(opk, E);
+      serial();
+      continue;
+    }
+    const u32 L = 63u - (u32)__builtin_clzll(S);
+    pos = readlane(succ, L);
+    op = readlane(opk + len, L);
+  }
+  return status;
+}
+
+__global__ __launch_bounds__(kBigWaves * 64) void lz4_index_big_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len,
+    const u32* __restrict__ out_len, i32* __restrict__ status_out, u32* __restrict__ counter,
+    const u32* __restrict__ big_list, const u32* __restrict__ bm_base, const u32* __restrict__ hdr,
+    u32* __restrict__ bitmap) {
+  __shared__ u32 ring_s[kBigWaves][kBigRingDw + 8];
+  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const u32 lane = threadIdx.x & 63;
+  const u32 count = counter[1];
+  if (count == 0) return;
+  for (;;) {  // lane 0 adds 1; its result is the index
+    const u32 got = atomicAdd(&counter[2], lane == 0 ? 1u : 0u);
+    const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
+    if (idx >= count) break;
+    const u32 m = (u32)__builtin_amdgcn_readfirstlane((int)big_list[idx]);
+    const i32 st = lz4_walk_big(m, in, in_off, in_len, out_len, bm_base, hdr, bitmap, ring_s[wv], lane);
+    if (lane == 0) status_out[m] = st;
+  }
 }
 
 // ===========================================================================
@@ -850,13 +1140,19 @@ extern "C" int fsg_debug_l4stamps(unsigned long long* out, int reset) {
 }
 #endif
 
-// Workspace: [0, 256) counters | bm_base[n] | hdr[n] | bitmap words
-// (round_up(ceil(block / 32), 4) per message <= total / 32 + 4 n).
+// Workspace: [0, 256) counters (0 bitmap words allocated, 1 large blocks
+// listed, 2 large blocks taken) | bm_base[n] | hdr[n] | big_list[n] | bitmap
+// words (round_up(ceil(block / 32), 4) per message <= total / 32 + 4 n).
 constexpr u64 kL4Head = 256;
 __host__ u64 l4_list_bytes(u32 n) { return ((u64)n * 4 + 255) & ~(u64)255; }
 size_t lz4_decode_workspace_bytes(u32 n_msgs, u64 total_in_bytes) {
-  return kL4Head + 2 * l4_list_bytes(n_msgs) + 4 * (total_in_bytes / 32 + 4 * (u64)n_msgs + 4);
+  return kL4Head + 3 * l4_list_bytes(n_msgs) + 4 * (total_in_bytes / 32 + 4 * (u64)n_msgs + 4);
 }
+// blocks above this many bytes take the wave walk (FSG_L4_BIG_MIN, read per
+// call: the tests lower it)
+constexpr u32 kL4BigMin = 65536;
+constexpr u32 kL4SmallBatch = 256;
+constexpr u32 kL4BigMinSmall = 2048;
 
 // Per-device event that orders the execution pass behind the index pass in
 // the two-stream form (created on first use; nullptr: one stream).
@@ -883,7 +1179,7 @@ hipError_t launch_lz4_decode2(const u8* in, const u64* in_off, const u32* in_len
                               const u64* out_off, const u32* out_cap, u32* out_len, i32* status, void* ws,
                               size_t ws_bytes, hipStream_t stream, hipStream_t pass1_stream) {
   if (n_msgs == 0) return hipSuccess;
-  const u64 fixed = kL4Head + 2 * l4_list_bytes(n_msgs);
+  const u64 fixed = kL4Head + 3 * l4_list_bytes(n_msgs);
   if (ws_bytes < fixed) return hipErrorInvalidValue;
   // Two-stream form (as launch_decode_v4's): the index pass on pass1_stream,
   // the execution and fallback passes on `stream` behind an event, so a
@@ -903,12 +1199,22 @@ hipError_t launch_lz4_decode2(const u8* in, const u64* in_off, const u32* in_len
   u32* counter = reinterpret_cast<u32*>(w);
   u32* bm_base = reinterpret_cast<u32*>(w + kL4Head);
   u32* hdr = reinterpret_cast<u32*>(w + kL4Head + l4_list_bytes(n_msgs));
+  u32* big_list = reinterpret_cast<u32*>(w + kL4Head + 2 * l4_list_bytes(n_msgs));
   u32* bitmap = reinterpret_cast<u32*>(w + fixed);
+  // a batch of at most kL4SmallBatch messages has the chip to itself: a
+  // wave per block is quicker than one lane per block from a few KiB on
+  const char* bm_env = getenv("FSG_L4_BIG_MIN");
+  const u32 big_min = bm_env ? (u32)strtoul(bm_env, nullptr, 10) : (n_msgs <= kL4SmallBatch ? kL4BigMinSmall : kL4BigMin);
   const u64 cap_words = (ws_bytes - fixed) / 16 * 4;  // whole 16-byte groups
   e = hipMemsetAsync(counter, 0, kL4Head, s1);
   if (e != hipSuccess) return e;
   lz4_index_kernel<<<(n_msgs + 63) / 64, 64, 0, s1>>>(in, in_off, in_len, n_msgs, out_cap, out_len, status,
-                                                      counter, bm_base, hdr, bitmap, cap_words);
+                                                      counter, bm_base, hdr, bitmap, cap_words, big_list, big_min);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // (a grid of 256 blocks: with no listed block each wave reads the count and leaves)
+  lz4_index_big_kernel<<<256, kBigWaves * 64, 0, s1>>>(in, in_off, in_len, out_len, status, counter, big_list,
+                                                       bm_base, hdr, bitmap);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (two) {

@@ -62,7 +62,8 @@ size_t fsg_lz4_decompress_workspace_bytes(uint32_t n_msgs, uint64_t total_in_byt
 
 /* fsg_lz4_decompress_batch (same arguments, statuses and bytes) on the
  * two-pass decoder: a lane-per-message index pass (validation + sequence
- * bitmap), then a wave-per-message execution pass.  Messages whose bitmap
+ * bitmap; blocks over 64 KiB, or over 2 KiB in batches of <= 256 messages,
+ * indexed by a wave each), then a wave-per-message execution pass.  Messages whose bitmap
  * does not fit the workspace, or every message when d_workspace is NULL or
  * smaller than fsg_lz4_decompress_workspace_bytes(n_msgs, 0), run the
  * one-pass kernel. */

@@ -41,8 +41,22 @@ def _header(n: int) -> bytes:
     return bytes(out)
 
 
-@pytest.fixture(params=[False, True], ids=["one_pass", "two_pass"])
-def two(request):
+@pytest.fixture(params=["one_pass", "two_pass", "two_pass_wave_walk"])
+def two(request, monkeypatch):
+    """one_pass: lz4.hip's lane kernel; two_pass: lz4_decode2.hip; with
+    _wave_walk, every block of more than 64 bytes is indexed by the wave walk
+    (lz4_index_big_kernel, normally for blocks of more than 64 KiB)."""
+    if request.param == "two_pass_wave_walk":
+        monkeypatch.setenv("FSG_L4_BIG_MIN", "64")
+    return request.param != "one_pass"
+
+
+@pytest.fixture(params=["lane_walk", "wave_walk"])
+def walk(request, monkeypatch):
+    """The index pass of the two-pass decoder: the lane walk, or (blocks of
+    more than 64 bytes) the wave walk."""
+    if request.param == "wave_walk":
+        monkeypatch.setenv("FSG_L4_BIG_MIN", "64")
     return request.param
 
 
@@ -136,7 +150,7 @@ def _kinds(rng, n):
     return out
 
 
-def test_lz4_two_pass_kinds_against_oracle(gpu, o):
+def test_lz4_two_pass_kinds_against_oracle(gpu, o, walk):
     """Compressor output of every kind and size (long literals of random
     bodies, long runs of zeros, short periods, text, JSON) through the
     two-pass decoder: bytes equal to the inputs, statuses OK."""
@@ -149,7 +163,7 @@ def test_lz4_two_pass_kinds_against_oracle(gpu, o):
         assert y == x, (i, len(x))
 
 
-def test_lz4_two_pass_synthetic_sequences(gpu, o):
+def test_lz4_two_pass_synthetic_sequences(gpu, o, walk):
     """Blocks built sequence by sequence (tests/lz4_blocks.py): every
     extension-byte boundary of both lengths, 255 runs, empty literals,
     offsets 1..15 / 16..1536 / above, matches longer than their offset and
@@ -166,7 +180,7 @@ def test_lz4_two_pass_synthetic_sequences(gpu, o):
         assert s == 0 and y == w, i
 
 
-def test_lz4_two_pass_workspace_garbage_and_fallback(gpu, o):
+def test_lz4_two_pass_workspace_garbage_and_fallback(gpu, o, walk):
     """The workspace may hold anything (filled with 0xff first), and one
     sized for less input than the batch sends the messages whose bitmap does
     not fit to the one-pass kernel: the same bytes and statuses either way."""
@@ -196,7 +210,7 @@ def test_lz4_two_pass_c3_like_batch(gpu, o):
     assert (st == 0).all() and all(y == x for y, x in zip(outs, xs))
 
 
-def test_lz4_two_stream_form(gpu, o):
+def test_lz4_two_stream_form(gpu, o, walk):
     """fsg_lz4_decompress_batch_2s: two batches with their own buffers,
     decoded alternately four times, each batch's index pass on a second
     stream beside the other's execution (the slot's previous execution
