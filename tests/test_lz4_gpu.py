@@ -41,22 +41,28 @@ def _header(n: int) -> bytes:
     return bytes(out)
 
 
-@pytest.fixture(params=["one_pass", "two_pass", "two_pass_wave_walk"])
+# FSG_L4_BIG_MIN per index-pass variant: the lane walk for every block, the
+# wave walk (lz4_index_big_kernel) for every block of more than 64 bytes
+_WALK_MIN = {"lane_walk": "4294967295", "wave_walk": "64"}
+
+
+@pytest.fixture(params=["one_pass", "two_pass", "two_pass_lane_walk", "two_pass_wave_walk"])
 def two(request, monkeypatch):
-    """one_pass: lz4.hip's lane kernel; two_pass: lz4_decode2.hip; with
-    _wave_walk, every block of more than 64 bytes is indexed by the wave walk
-    (lz4_index_big_kernel, normally for blocks of more than 64 KiB)."""
-    if request.param == "two_pass_wave_walk":
-        monkeypatch.setenv("FSG_L4_BIG_MIN", "64")
+    """one_pass: lz4.hip's lane kernel; two_pass: lz4_decode2.hip at its
+    default thresholds (the wave walk for blocks over 64 KiB, over 2 KiB in
+    batches of <= 256 messages); _lane_walk / _wave_walk force one index
+    pass for every block."""
+    for k, v in _WALK_MIN.items():
+        if request.param.endswith(k):
+            monkeypatch.setenv("FSG_L4_BIG_MIN", v)
     return request.param != "one_pass"
 
 
 @pytest.fixture(params=["lane_walk", "wave_walk"])
 def walk(request, monkeypatch):
-    """The index pass of the two-pass decoder: the lane walk, or (blocks of
-    more than 64 bytes) the wave walk."""
-    if request.param == "wave_walk":
-        monkeypatch.setenv("FSG_L4_BIG_MIN", "64")
+    """The index pass of the two-pass decoder forced for every block: the
+    lane walk, or (blocks of more than 64 bytes) the wave walk."""
+    monkeypatch.setenv("FSG_L4_BIG_MIN", _WALK_MIN[request.param])
     return request.param
 
 
