@@ -18,6 +18,9 @@
 //     offsets alternate, so bit 2i is token i and bit 2i+1 its offset.  Input
 //     through a per-lane LDS ring of 16-byte chunks (loads one iteration ahead
 //     of the parse), bits through a per-lane LDS ring of 128-byte groups.
+//     Blocks over big_min bytes are listed instead and indexed by
+//     lz4_index_big_kernel, a wave per block (pointer doubling over 64-byte
+//     windows, as the Snappy pass 1b).
 //
 //   pass 2, lz4_exec_kernel (one WAVE per message): takes up to 64 sequences
 //     per group, one per lane.  From the three positions T (token), O (offset

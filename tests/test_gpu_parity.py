@@ -126,8 +126,8 @@ def test_randomized_against_oracle(gpu, oracle, encoder):
 @pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1"), (0, "1p")])
 def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, monkeypatch):
     """Mutated and truncated streams (64 B to 70 KB bodies).  fork "1" runs
-    the path of batches over 128K messages: plan pass, side stream, and
-    bodies of <= 1 KiB output decoded one per lane; "1p" with the small
+    the path of batches over 128K messages: plan pass, the large messages'
+    passes on side streams, the small ones on a persistent grid; "1p" with the small
     messages' execution grid shrunk to 5 blocks, so each wave loops over
     ~150 messages (FSG_SMALL_PERSIST)."""
     monkeypatch.setenv("FSG_DECODE_FORK", fork[0])
