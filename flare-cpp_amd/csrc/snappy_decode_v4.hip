@@ -327,7 +327,7 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     u32* __restrict__ bm_counter, u32* __restrict__ bm_base_out,
     u32* __restrict__ bitmap, u64 bm_capacity_words, u32* __restrict__ big_count,
     u32* __restrict__ big_list, u32 big_threshold, const u32* __restrict__ walk_perm,
-    const u32* __restrict__ walk_hist) {
+    const u32* __restrict__ walk_hist, u32 walk_part = 0, u32 split_class = 0) {
   // Lean geometry (the two-stream form, whose walk runs beside the previous
   // batch's execution pass in the CU resources that pass leaves free: <= 80
   // VGPRs, 12.3 KB of LDS): an 8-chunk input ring, 16 tags per iteration, 4
@@ -380,10 +380,14 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   // planned with a walk order: lane g walks message walk_perm[g], the
   // messages grouped by size class so a wave's lanes finish together
   const u32 gid = blockIdx.x * blockDim.x + threadIdx.x;
+  // (walk_part 1 / 2: only the walk order's positions below / from the
+  // first one of class split_class -- the larger / the smaller bodies)
   const bool ordered = kPlanned && walk_perm;
   const u32 n_walk = ordered ? walk_hist[2 * kWalkClasses] : n_msgs;
-  const bool valid_msg = gid < n_walk;
-  const u32 m = ordered ? (valid_msg ? walk_perm[gid] : 0u) : gid;
+  const u32 split = walk_part ? walk_hist[kWalkClasses + split_class] : 0u;
+  const u32 w_lo = walk_part == 2 ? split : 0u, w_hi = walk_part == 1 ? split : n_walk;
+  const bool valid_msg = ordered ? gid < w_hi - w_lo : gid < n_walk;
+  const u32 m = ordered ? (valid_msg ? walk_perm[w_lo + gid] : 0u) : gid;
 
   const u8* ib = valid_msg ? in + in_off[m] : in;
   const u32 n_in = valid_msg ? in_len[m] : 0u;
@@ -2347,7 +2351,8 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     u32* __restrict__ bitmap, const u32* __restrict__ seg_list,
     const u32* __restrict__ seg_count, const u32* __restrict__ whole_list,
     const u32* __restrict__ whole_count, u32* __restrict__ exec_next, u32 big_blocks,
-    u32 big_threshold, u32 prio, u32 keep_hist, u32 small_stride) {
+    u32 big_threshold, u32 prio, u32 keep_hist, u32 small_stride, const u32* __restrict__ walk_perm = nullptr,
+    const u32* __restrict__ walk_hist = nullptr, u32 walk_part = 0, u32 split_class = 0) {
   // per wave: the tag ring, then the output window
   __shared__ __attribute__((aligned(16))) u8 wl_s[kWavesPerBlock][4 * kTagRing + kWindow + 32];
   __shared__ __attribute__((aligned(16))) u8 pmap_s[kWavesPerBlock][V == 5 ? 1 : kMaxPieces];
@@ -2386,6 +2391,18 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
     // (the forked path's batches of mostly small bodies)
     const u32 m0 = (blockIdx.x - big_blocks) * kWavesPerBlock + wv;
     const u32 step = small_stride ? small_stride * kWavesPerBlock : 0xffffffffu;
+    if (walk_perm) {
+      // the messages in walk order (forked path): positions [lo, hi) of
+      // walk_perm -- part 1 / 2 the larger / smaller bodies, 3 all of them
+      const u32 n_walk = walk_hist[2 * kWalkClasses];
+      const u32 split = walk_hist[kWalkClasses + split_class];
+      const u32 lo = walk_part == 2 ? split : 0u, hi = walk_part == 1 ? split : n_walk;
+      for (u32 i = m0; i < hi - lo; i = i + step < i ? 0xffffffffu : i + step) {
+        const u32 m = walk_perm[lo + i];
+        run(m, ring, pmap, sb, lane, status[m], 0u, 0u, out_len[m]);
+      }
+      return;
+    }
     for (u32 m = m0; m < n_msgs; m = m + step < m ? 0xffffffffu : m + step)
       if (in_len[m] <= big_threshold) run(m, ring, pmap, sb, lane, status[m], 0u, 0u, out_len[m]);
     return;
@@ -2511,6 +2528,8 @@ struct SideStream {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // the huge messages' pass 1b + execution (nullptr: not created)
   hipEvent_t join2 = nullptr;
+  hipStream_t stream3 = nullptr;  // the larger small bodies' walk + execution (split walk)
+  hipEvent_t join3 = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   hipEvent_t pass1 = nullptr;  // two-stream calls: pass 1 done (fsg_decompress_batch_2s)
   std::mutex mu;
@@ -2532,6 +2551,9 @@ static SideStream* side_stream() {
     if (s->stream && (hipStreamCreateWithFlags(&s->stream2, hipStreamNonBlocking) != hipSuccess ||
                       hipEventCreateWithFlags(&s->join2, hipEventDisableTiming) != hipSuccess))
       s->stream2 = nullptr;
+    if (s->stream && (hipStreamCreateWithFlags(&s->stream3, hipStreamNonBlocking) != hipSuccess ||
+                      hipEventCreateWithFlags(&s->join3, hipEventDisableTiming) != hipSuccess))
+      s->stream3 = nullptr;
   });
   return s->stream ? s : nullptr;
 }
@@ -2648,11 +2670,32 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   if (n_msgs <= kSmallBatch) thr = 0;
   const u32 big_threshold = (u32)thr;
   const u32 idx_blocks = (n_msgs + 64 * kIdxWaves - 1) / (64 * kIdxWaves);
-  auto launch_index = [&](bool planned) -> hipError_t {
+  // Split walk (forked path, FSG_SPLIT_WALK, read per call): the size-ordered
+  // lane walk in two launches on two streams -- bodies of class >=
+  // kSplitClass (compressed size < 2^(15 - kSplitClass) bytes) on the main
+  // stream, whose execution then starts without waiting for the larger
+  // bodies' longer walks, which run with their execution on a third stream.
+  // FSG_SPLIT_WALK (read per call, A/B): 0 the execution in message order
+  // after one walk; 1 the walk and execution split on two streams (above);
+  // 2 one walk, then the execution in walk order (size classes, largest
+  // first); 3 (default) one walk, then the smaller bodies' execution, then
+  // the larger ones'.  CM, A/B on one box, two rounds, with the chunked
+  // huge-body walk: 0 6.74 / 6.72, 1 (unchunked) 7.54 / 7.45 -- the third
+  // stream shares a hardware queue with the huge bodies' stream and waits
+  // behind it --, 2 6.55 / 6.45, 3 6.45 / 6.44 ms.  In message order a
+  // wave's run of bodies mixes sizes and the launch waits for the waves that
+  // drew the larger ones (execution 4.66 ms; in walk order 3.91).
+  const char* sw_env = getenv("FSG_SPLIT_WALK");
+  const u32 split_mode = sw_env ? (u32)atoi(sw_env) : 3u;
+  const bool split_walk = split_mode == 1;
+  const char* sc_env = getenv("FSG_SPLIT_CLASS");
+  const u32 kSplitClass = sc_env ? (u32)atoi(sc_env) % kWalkClasses : 4u;
+  auto launch_index = [&](bool planned, hipStream_t st = nullptr, u32 part = 0) -> hipError_t {
     if (planned)
-      index_kernel<true><<<idx_blocks, 64 * kIdxWaves, 0, stream>>>(
+      index_kernel<true><<<idx_blocks, 64 * kIdxWaves, 0, st ? st : stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
-          cap_words, big_count, big_list, big_threshold, kWalkOrder ? walk_perm : nullptr, walk_hist);
+          cap_words, big_count, big_list, big_threshold, kWalkOrder ? walk_perm : nullptr, walk_hist, part,
+          kSplitClass);
     else if (two && kLeanWalk)
       index_kernel<false, true><<<idx_blocks, 64 * kIdxWaves, idx_lean_lds_bytes(), stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
@@ -2740,15 +2783,18 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     ek<<<fork_big_blocks, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(b.seg_list), b.seg_count, b.whole_list, b.whole_count, b.exec_next,
-        fork_big_blocks, big_threshold, 0u, keep_hist, 0u);
+        fork_big_blocks, big_threshold, 0u, keep_hist, 0u, nullptr, nullptr, 0u, 0u);
     return hipGetLastError();
   };
   // The huge messages' pass 1b, chunked (chunk_*_kernel): when the record
   // region holds a batch of this workspace's size (FSG_CHUNKED_HUGE=0: one
-  // wave per message as before).
+  // wave per message).  On by default since the small bodies' execution runs
+  // in walk order (FSG_SPLIT_WALK 3): CM 6.77-6.81 -> 6.44 ms, where the
+  // chunked walk alone had measured slower (the huge bodies were then off
+  // the critical path).
   const bool kChunked = [] {  // (read per call: the tests run both forms)
     const char* e = getenv("FSG_CHUNKED_HUGE");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   const u64 max_huge = chunk_bytes / 320;
   const u64 max_recs = max_huge ? (chunk_bytes - 8 * max_huge) / sizeof(ChunkRec) : 0;
@@ -2780,7 +2826,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     ek<<<fork_big_blocks, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(b.seg_list), b.seg_count, b.whole_list, b.whole_count, b.exec_next,
-        fork_big_blocks, big_threshold, 0u, keep_hist, 0u);
+        fork_big_blocks, big_threshold, 0u, keep_hist, 0u, nullptr, nullptr, 0u, 0u);
     return hipGetLastError();
   };
   // The forked path's small-message launch: a grid of kSmallPersist blocks
@@ -2792,14 +2838,16 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     const char* e = getenv("FSG_SMALL_PERSIST");
     return e ? (u32)atoi(e) : 1792u;
   }();
-  auto launch_small = [&](hipStream_t st) -> hipError_t {
+  auto launch_small = [&](hipStream_t st, u32 part) -> hipError_t {
     // one wave per message; large ones are skipped (big_blocks = 0: no block
-    // takes the large-message role)
+    // takes the large-message role).  part 1 / 2: the messages of that part
+    // of the split walk, in walk order.
     const u32 grid = kSmallPersist && kSmallPersist < small_blocks ? kSmallPersist : small_blocks;
     ek<<<grid, kWavesPerBlock * 64, 0, st>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), set0.seg_count, whole_list, set0.whole_count, set0.exec_next,
-        0u, big_threshold, 0u, keep_hist, grid < small_blocks ? grid : 0u);
+        0u, big_threshold, 0u, keep_hist, grid < small_blocks ? grid : 0u, part ? walk_perm : nullptr,
+        part ? walk_hist : nullptr, part, kSplitClass);
     return hipGetLastError();
   };
   SideStream* side = fork ? side_stream() : nullptr;
@@ -2832,8 +2880,27 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     }
     if ((e = launch_big(side->stream, set0, split ? 2u : 0u)) != hipSuccess) return e;
     if ((e = hipEventRecord(side->join, side->stream)) != hipSuccess) return e;
-    if ((e = launch_index(true)) != hipSuccess) return e;
-    if ((e = launch_small(stream)) != hipSuccess) return e;
+    const bool three = split_walk && kWalkOrder && side->stream3;
+    if (three) {
+      // the larger small bodies: walk and execution on the third stream
+      if ((e = hipStreamWaitEvent(side->stream3, side->fork, 0)) != hipSuccess) return e;
+      if ((e = launch_index(true, side->stream3, 1u)) != hipSuccess) return e;
+      if ((e = launch_small(side->stream3, 1u)) != hipSuccess) return e;
+      if ((e = hipEventRecord(side->join3, side->stream3)) != hipSuccess) return e;
+      if ((e = launch_index(true, stream, 2u)) != hipSuccess) return e;
+      if ((e = launch_small(stream, 2u)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(stream, side->join3, 0)) != hipSuccess) return e;
+    } else {
+      if ((e = launch_index(true)) != hipSuccess) return e;
+      if (kWalkOrder && split_mode == 2) {
+        if ((e = launch_small(stream, 3u)) != hipSuccess) return e;
+      } else if (kWalkOrder && split_mode == 3) {
+        if ((e = launch_small(stream, 2u)) != hipSuccess) return e;
+        if ((e = launch_small(stream, 1u)) != hipSuccess) return e;
+      } else {
+        if ((e = launch_small(stream, 0u)) != hipSuccess) return e;
+      }
+    }
     if ((e = hipStreamWaitEvent(stream, side->join, 0)) != hipSuccess) return e;
     if (split && (e = hipStreamWaitEvent(stream, side->join2, 0)) != hipSuccess) return e;
   } else {
@@ -2851,7 +2918,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     ek<<<big_blocks + small_blocks, kWavesPerBlock * 64, 0, stream>>>(
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), set0.seg_count, whole_list, set0.whole_count, set0.exec_next,
-        big_blocks, big_threshold, kPrio, keep_hist, 0u);
+        big_blocks, big_threshold, kPrio, keep_hist, 0u, nullptr, nullptr, 0u, 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // Diagnostic only (FSG_DIAG_NO_TAIL=1): skip this pass to trace the

@@ -123,15 +123,20 @@ def test_randomized_against_oracle(gpu, oracle, encoder):
     assert (st == 0).all() and all(o == x for o, x in zip(outs, items))
 
 
-@pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1"), (0, "1p")])
+@pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1"), (0, "1p"), (0, "1s0"),
+                                          (0, "1s1"), (0, "1s2")])
 def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, monkeypatch):
     """Mutated and truncated streams (64 B to 70 KB bodies).  fork "1" runs
     the path of batches over 128K messages: plan pass, the large messages'
     passes on side streams, the small ones on a persistent grid; "1p" with the small
     messages' execution grid shrunk to 5 blocks, so each wave loops over
-    ~150 messages (FSG_SMALL_PERSIST)."""
+    ~150 messages (FSG_SMALL_PERSIST); "1sK" with FSG_SPLIT_WALK=K (0: the
+    small bodies executed in message order; 1: walk and execution split by
+    size on two streams; 2: one execution launch in walk order; default 3:
+    two execution launches by size)."""
     monkeypatch.setenv("FSG_DECODE_FORK", fork[0])
     monkeypatch.setenv("FSG_SMALL_PERSIST", "5" if fork == "1p" else "1792")
+    monkeypatch.setenv("FSG_SPLIT_WALK", fork[2] if fork.startswith("1s") else "3")
     gpu.codec.select_kernels(variant, 0)
     rng = np.random.default_rng(9)
     srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (64, 700, 9000, 70000)]
