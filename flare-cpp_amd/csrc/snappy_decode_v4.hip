@@ -2670,11 +2670,9 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   if (n_msgs <= kSmallBatch) thr = 0;
   const u32 big_threshold = (u32)thr;
   const u32 idx_blocks = (n_msgs + 64 * kIdxWaves - 1) / (64 * kIdxWaves);
-  // Split walk (forked path, FSG_SPLIT_WALK, read per call): the size-ordered
-  // lane walk in two launches on two streams -- bodies of class >=
-  // kSplitClass (compressed size < 2^(15 - kSplitClass) bytes) on the main
-  // stream, whose execution then starts without waiting for the larger
-  // bodies' longer walks, which run with their execution on a third stream.
+  // Order of the forked path's small-message execution.  The split point:
+  // bodies of size class >= kSplitClass (compressed size < 2^(16 -
+  // kSplitClass) bytes; FSG_SPLIT_CLASS) vs the larger ones.
   // FSG_SPLIT_WALK (read per call, A/B): 0 the execution in message order
   // after one walk; 1 the walk and execution split on two streams (above);
   // 2 one walk, then the execution in walk order (size classes, largest
