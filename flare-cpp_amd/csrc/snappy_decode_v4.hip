@@ -2764,13 +2764,15 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     return hipGetLastError();
   };
   auto launch_index_big = [&](hipStream_t st) -> hipError_t { return launch_index_big_set(st, set0, 0u); };
-  // The forked path's large-message launch runs alone once the lane walk's
-  // side finishes, so it takes a full machine of blocks (7 per CU): CM 9.9 ->
-  // 8.85 ms against 512 blocks (A/B on one box, twice; 4096: 8.86).
+  // The forked path's large-message launches: CM 9.9 -> 8.85 ms with 1,792
+  // blocks against 512 when they ran alone after the lane walk; 1,024 since
+  // the small bodies' execution (walk order, 3,584 blocks) runs beside them:
+  // CM 6.32-6.37 -> 6.20-6.25 ms for the two grid sizes together (A/B on one
+  // box, four rounds).
   static const u32 kBigBlocksFork = [] {  // A/B knob, separate from the one-stream launch's
     const char* e = getenv("FSG_EXEC_BIG_BLOCKS_FORK");
-    const int v = e ? atoi(e) : 1792;
-    return v >= 1 ? (u32)v : 1792u;
+    const int v = e ? atoi(e) : 1024;
+    return v >= 1 ? (u32)v : 1024u;
   }();
   auto launch_big = [&](hipStream_t st, const BigSet& b, u32 mode) -> hipError_t {
     hipError_t e2 = launch_index_big_set(st, b, mode);
@@ -2827,14 +2829,15 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
         fork_big_blocks, big_threshold, 0u, keep_hist, 0u, nullptr, nullptr, 0u, 0u);
     return hipGetLastError();
   };
-  // The forked path's small-message launch: a grid of kSmallPersist blocks
-  // (7 waves per SIMD), each wave looping over messages; CM 7.31 -> 7.02 ms
-  // against one wave per message (A/B on one box, two passes; 1,024 blocks:
-  // 7.11, 3,584: 7.03).  FSG_SMALL_PERSIST (blocks, read per call: the tests
-  // shrink it; 0 = one wave per message).
+  // The forked path's small-message launches: a grid of kSmallPersist blocks,
+  // each wave looping over messages; CM 7.31 -> 7.02 ms against one wave per
+  // message (A/B on one box, two passes; 1,024 blocks: 7.11, 3,584: 7.03);
+  // 3,584 (two rounds of blocks at 7 waves per SIMD) since the execution
+  // runs in walk order (see kBigBlocksFork).  FSG_SMALL_PERSIST (blocks, read
+  // per call: the tests shrink it; 0 = one wave per message).
   const u32 kSmallPersist = [] {
     const char* e = getenv("FSG_SMALL_PERSIST");
-    return e ? (u32)atoi(e) : 1792u;
+    return e ? (u32)atoi(e) : 3584u;
   }();
   auto launch_small = [&](hipStream_t st, u32 part) -> hipError_t {
     // one wave per message; large ones are skipped (big_blocks = 0: no block
