@@ -8,6 +8,7 @@
 
 #include "../../include/flare_lz4_gpu.h"
 #include "../../include/flare_snappy_gpu.h"
+#include "options.h"
 #include "snappy_device.h"
 
 namespace fsg {
@@ -58,6 +59,49 @@ int env_int(const char* name) {
   const char* e = getenv(name);
   return e ? atoi(e) : 0;
 }
+
+// ---- the option table (csrc/options.h): name, environment variable, default
+struct OptDesc {
+  const char* name;
+  const char* env;
+  int64_t dflt;
+};
+constexpr OptDesc kOptDesc[fsg::kOptCount] = {
+    {"decode_fork", "FSG_DECODE_FORK", -1},
+    {"split_walk", "FSG_SPLIT_WALK", 3},
+    {"split_class", "FSG_SPLIT_CLASS", 4},
+    {"exec_keep", "FSG_EXEC_KEEP", -1},
+    {"chunked_huge", "FSG_CHUNKED_HUGE", 1},
+    {"small_persist", "FSG_SMALL_PERSIST", 3584},
+    {"small_batch", "FSG_SMALL_BATCH", 64},
+    {"split_huge", "FSG_SPLIT_HUGE", 1},
+    {"walk_order", "FSG_WALK_ORDER", 1},
+    {"lean_walk", "FSG_LEAN_WALK", 1},
+    {"exec_big_blocks", "FSG_EXEC_BIG_BLOCKS", 512},
+    {"exec_prio", "FSG_EXEC_PRIO", 1},
+    {"exec_big_blocks_fork", "FSG_EXEC_BIG_BLOCKS_FORK", 1024},
+    {"diag_no_tail", "FSG_DIAG_NO_TAIL", 0},
+    {"encode_wave_min", "FSG_ENCODE_WAVE_MIN", 16384},
+    {"encode_wave_share", "FSG_ENCODE_WAVE_SHARE", 280},
+    {"encode_wave_all_mb", "FSG_ENCODE_WAVE_ALL_MB", 640},
+    {"encode_lanes", "FSG_ENCODE_LANES", 0},
+    {"lz4_big_min", "FSG_L4_BIG_MIN", -1},
+};
+std::atomic<int64_t> g_opt[fsg::kOptCount];
+// the environment, once, when the library is loaded
+[[maybe_unused]] const bool g_opt_init = [] {
+  for (int i = 0; i < fsg::kOptCount; ++i) {
+    const char* e = getenv(kOptDesc[i].env);
+    g_opt[i].store(e && *e ? strtoll(e, nullptr, 10) : kOptDesc[i].dflt);
+  }
+  return true;
+}();
+int find_opt(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < fsg::kOptCount; ++i)
+    if (strcmp(name, kOptDesc[i].name) == 0) return i;
+  return -1;
+}
 // Kernel variants (0 = automatic).  Initialised from FSG_DECODE_KERNEL /
 // FSG_ENCODE_KERNEL, changeable with fsg_select_kernels for A/B runs.
 std::atomic<int> g_decode_variant{env_int("FSG_DECODE_KERNEL")};
@@ -65,12 +109,12 @@ std::atomic<int> g_encode_variant{env_int("FSG_ENCODE_KERNEL")};
 // Messages of at least this many bytes (and every fragment of a message over
 // 64 KiB) form the long list, whose units the wave encoder (hash table in
 // LDS, one wave per fragment) and the lane encoder share (wave_quota); the
-// shorter messages go to the lane encoder.  FSG_ENCODE_WAVE_MIN overrides
-// per call (0 = lane encoder only).  Measured on MI355X (A/B, one box): C3
+// shorter messages go to the lane encoder.  Option encode_wave_min
+// (FSG_ENCODE_WAVE_MIN; 0 = lane encoder only).  Measured on MI355X (A/B, one box): C3
 // compress 108.0 -> 98.4 ms, C5 54.9 -> 39.1 ms.
 fsg::u32 encode_wave_min() {
-  const char* e = getenv("FSG_ENCODE_WAVE_MIN");
-  return e ? (fsg::u32)atoi(e) : 16384u;
+  const int64_t v = fsg::opt(fsg::kOptEncodeWaveMin);
+  return v >= 0 ? (fsg::u32)v : 16384u;
 }
 // Test knob: cap the staging region of a split message's fragments (bytes;
 // 0 = slot / fragments).  Small caps force the whole-message fallback pass.
@@ -83,7 +127,30 @@ int record(hipError_t e, const char* where) {
 }
 }  // namespace
 
+int64_t fsg::opt(fsg::Opt o) { return g_opt[o].load(std::memory_order_relaxed); }
+
 extern "C" {
+
+int fsg_set_option(const char* name, int64_t value) {
+  const int i = find_opt(name);
+  if (i < 0) return FSG_ERR_INVALID_ARG;
+  g_opt[i].store(value, std::memory_order_relaxed);
+  return FSG_SUCCESS;
+}
+
+int fsg_get_option(const char* name, int64_t* value) {
+  const int i = find_opt(name);
+  if (i < 0 || !value) return FSG_ERR_INVALID_ARG;
+  *value = g_opt[i].load(std::memory_order_relaxed);
+  return FSG_SUCCESS;
+}
+
+int fsg_default_option(const char* name, int64_t* value) {
+  const int i = find_opt(name);
+  if (i < 0 || !value) return FSG_ERR_INVALID_ARG;
+  *value = kOptDesc[i].dflt;
+  return FSG_SUCCESS;
+}
 
 const char* fsg_version(void) { return "flare-snappy-gpu 0.1 gfx950"; }
 
@@ -182,7 +249,7 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
     const fsg::u32 cap = max_in_len == 0 || max_in_len > fsg::kBlockSize ? fsg::kBlockSize : max_in_len;
     // Lanes in flight (tuning knob): fewer lanes keep their tables and
     // recent input cache-resident; each lane then encodes more messages.
-    static const unsigned lanes_cap = (unsigned)env_int("FSG_ENCODE_LANES");
+    const unsigned lanes_cap = (unsigned)fsg::opt(fsg::kOptEncodeLanes);
     if (lanes_cap && lanes_cap < slots) slots = (lanes_cap + 63) / 64 * 64;
     return record(fsg::launch_encode_v3(d_in, d_in_off, d_in_len, n_msgs, max_in_len, d_out,
                                         d_out_off, d_out_len, d_status, d_workspace,

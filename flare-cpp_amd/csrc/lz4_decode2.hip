@@ -44,6 +44,7 @@
 #include <cstdlib>
 #include <mutex>
 
+#include "options.h"
 #include "wave_util.h"
 
 namespace fsg {
@@ -1206,8 +1207,10 @@ hipError_t launch_lz4_decode2(const u8* in, const u64* in_off, const u32* in_len
   u32* bitmap = reinterpret_cast<u32*>(w + fixed);
   // a batch of at most kL4SmallBatch messages has the chip to itself: a
   // wave per block is quicker than one lane per block from a few KiB on
-  const char* bm_env = getenv("FSG_L4_BIG_MIN");
-  const u32 big_min = bm_env ? (u32)strtoul(bm_env, nullptr, 10) : (n_msgs <= kL4SmallBatch ? kL4BigMinSmall : kL4BigMin);
+  // (option lz4_big_min overrides, -1 = this rule)
+  const i64 bm_opt = opt(kOptLz4BigMin);
+  const u32 big_min = bm_opt >= 0 && bm_opt <= 0xffffffffll ? (u32)bm_opt
+                                                            : (n_msgs <= kL4SmallBatch ? kL4BigMinSmall : kL4BigMin);
   const u64 cap_words = (ws_bytes - fixed) / 16 * 4;  // whole 16-byte groups
   e = hipMemsetAsync(counter, 0, kL4Head, s1);
   if (e != hipSuccess) return e;

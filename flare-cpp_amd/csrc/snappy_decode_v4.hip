@@ -36,6 +36,7 @@
 //
 // A message whose bitmap does not fit the workspace gets status kNeedFallback
 // in pass 1 and is decoded serially by one lane in pass 3 (fallback_kernel).
+#include "options.h"
 #include "snappy_lane_decode.h"
 #include "snappy_pieces.h"
 #include "wave_util.h"
@@ -2589,14 +2590,9 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   }
   hipStream_t const caller_stream = stream;
   // planned lane walk in size-class order (FSG_WALK_ORDER=0 disables)
-  static const bool kSplitHuge = [] {  // FSG_SPLIT_HUGE=0: one side stream
-    const char* e = getenv("FSG_SPLIT_HUGE");
-    return !(e && e[0] == '0');
-  }();
-  static const bool kWalkOrder = [] {
-    const char* e = getenv("FSG_WALK_ORDER");
-    return !(e && e[0] == '0');
-  }();
+  // (options: csrc/options.h, set with fsg_set_option; never the environment here)
+  const bool kSplitHuge = opt(kOptSplitHuge) != 0;  // 0: one side stream
+  const bool kWalkOrder = opt(kOptWalkOrder) != 0;
   // Two-stream form: the lean lane walk (FSG_LEAN_WALK=0: the standard one).
   // Measured (C3, stream of two alternating batches, one box): lean 6.13 ms
   // per batch, standard 6.57, serial 6.15; an execution pass made persistent
@@ -2605,16 +2601,16 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   // pass held to six blocks per CU by padding its LDS, with a two-wave lean
   // walk in the space left: 6.32 vs serial 6.11 (the walk's instructions
   // compete with an execution pass already at the issue limit).
-  static const bool kLeanWalk = [] {
-    const char* e = getenv("FSG_LEAN_WALK");
-    return !(e && e[0] == '0');
-  }();
+  const bool kLeanWalk = opt(kOptLeanWalk) != 0;
   if (two) stream = pass1_stream;  // every pass-1 launch below goes there
   // pass 2: one tag per lane (5) or <= 16-byte pieces per lane (4)
   auto* const ek = exec_variant == 4 ? &exec_kernel<4> : &exec_kernel<5>;
   u8* w = static_cast<u8*>(ws);
   const u64 base_bytes = (4ull * n_msgs + 255) & ~255ull;
-  if (ws_bytes < 256 + kListBases * base_bytes + 4 * 64) return hipErrorInvalidValue;
+  // the fixed part, the chunk-record region and a bitmap of at least the
+  // per-message minimum (decode_v4_workspace_bytes with no input): below it
+  // the region arithmetic below would underflow
+  if (ws_bytes < decode_v4_workspace_bytes(n_msgs, 0)) return hipErrorInvalidValue;
   u32* counter = reinterpret_cast<u32*>(w + kWsBmCounter);
   u32* big_count = reinterpret_cast<u32*>(w + kWsBigCount);
   u32* bm_base = reinterpret_cast<u32*>(w + 256);
@@ -2662,18 +2658,15 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   // batches): the lane walk would be one lane per message, its latency the
   // longest message's tag chain (~160 us for a 4 KiB text body), where pass
   // 1b walks each message with a whole wave (a few us).  Every message goes
-  // to pass 1b (FSG_SMALL_BATCH sets the bound; 0 disables).
-  static const u32 kSmallBatch = [] {
-    const char* e = getenv("FSG_SMALL_BATCH");
-    return e ? (u32)atoi(e) : 64u;
-  }();
-  if (n_msgs <= kSmallBatch) thr = 0;
+  // to pass 1b (option small_batch sets the bound; 0 disables).
+  const i64 kSmallBatch = opt(kOptSmallBatch);
+  if ((i64)n_msgs <= kSmallBatch) thr = 0;
   const u32 big_threshold = (u32)thr;
   const u32 idx_blocks = (n_msgs + 64 * kIdxWaves - 1) / (64 * kIdxWaves);
   // Order of the forked path's small-message execution.  The split point:
   // bodies of size class >= kSplitClass (compressed size < 2^(16 -
-  // kSplitClass) bytes; FSG_SPLIT_CLASS) vs the larger ones.
-  // FSG_SPLIT_WALK (read per call, A/B): 0 the execution in message order
+  // kSplitClass) bytes; option split_class) vs the larger ones.
+  // Option split_walk (A/B): 0 the execution in message order
   // after one walk; 1 the walk and execution split on two streams (above);
   // 2 one walk, then the execution in walk order (size classes, largest
   // first); 3 (default) one walk, then the smaller bodies' execution, then
@@ -2683,11 +2676,9 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   // behind it --, 2 6.55 / 6.45, 3 6.45 / 6.44 ms.  In message order a
   // wave's run of bodies mixes sizes and the launch waits for the waves that
   // drew the larger ones (execution 4.66 ms; in walk order 3.91).
-  const char* sw_env = getenv("FSG_SPLIT_WALK");
-  const u32 split_mode = sw_env ? (u32)atoi(sw_env) : 3u;
+  const u32 split_mode = (u32)opt(kOptSplitWalk);
   const bool split_walk = split_mode == 1;
-  const char* sc_env = getenv("FSG_SPLIT_CLASS");
-  const u32 kSplitClass = sc_env ? (u32)atoi(sc_env) % kWalkClasses : 4u;
+  const u32 kSplitClass = (u32)opt(kOptSplitClass) % kWalkClasses;
   auto launch_index = [&](bool planned, hipStream_t st = nullptr, u32 part = 0) -> hipError_t {
     if (planned)
       index_kernel<true><<<idx_blocks, 64 * kIdxWaves, 0, st ? st : stream>>>(
@@ -2717,28 +2708,22 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   // the fallback pass.
   // Only for batches of > 128K messages (the mixed-size ones): a fork and
   // join cost ~10 us (C2 0.159 -> 0.169 ms), and uniform batches send nothing
-  // to pass 1b (CM 14.4 -> 12.1 ms).  FSG_DECODE_FORK=0/1 forces (A/B).
+  // to pass 1b (CM 14.4 -> 12.1 ms).  Option decode_fork 0/1 forces (A/B).
   const u32 small_blocks = (n_msgs + kWavesPerBlock - 1) / kWavesPerBlock;
-  static const u32 kBigBlocks = [] {  // A/B knob
-    // at least one block: the large-message lists are only drained there
-    const char* e = getenv("FSG_EXEC_BIG_BLOCKS");
-    const int v = e ? atoi(e) : 512;
-    return v >= 1 ? (u32)v : 512u;
-  }();
-  static const u32 kPrio = [] {  // A/B knob: FSG_EXEC_PRIO=0 disables the priority raise
-    const char* e = getenv("FSG_EXEC_PRIO");
-    return e && e[0] == '0' ? 0u : 1u;
-  }();
-  // history kept when an exec window slides (FSG_EXEC_KEEP, read per call:
-  // the tests shrink it to exercise the slide's flush rule; 512..kMaxKeep
-  // bytes, a multiple of 16)
+  // A/B knob; at least one block: the large-message lists are only drained there
+  const i64 big_opt = opt(kOptExecBigBlocks);
+  const u32 kBigBlocks = big_opt >= 1 && big_opt <= (1 << 20) ? (u32)big_opt : 512u;
+  const u32 kPrio = opt(kOptExecPrio) != 0 ? 1u : 0u;  // A/B knob: 0 disables the priority raise
+  // history kept when an exec window slides (option exec_keep: the tests
+  // shrink it to exercise the slide's flush rule; 512..kMaxKeep bytes, a
+  // multiple of 16; anything else is the default)
   u32 keep_hist = kKeep;
-  if (const char* ke = getenv("FSG_EXEC_KEEP")) {
-    const int v = atoi(ke);
-    if (v >= 512 && v <= (int)kMaxKeep && v % 16 == 0) keep_hist = (u32)v;
+  {
+    const i64 v = opt(kOptExecKeep);
+    if (v >= 512 && v <= (i64)kMaxKeep && v % 16 == 0) keep_hist = (u32)v;
   }
-  const char* fork_env = getenv("FSG_DECODE_FORK");  // read per call: tests set it
-  const bool fork = !two && (fork_env ? atoi(fork_env) != 0 : n_msgs > 131072u);
+  const i64 fork_opt = opt(kOptDecodeFork);
+  const bool fork = !two && (fork_opt >= 0 ? fork_opt != 0 : n_msgs > 131072u);
   const u32 big_blocks = small_blocks < kBigBlocks ? small_blocks : kBigBlocks;
   // pass 1b: large messages, one wave each (an empty list costs one short
   // launch); they land in pass 2's work lists.  set 0: every large message
@@ -2769,11 +2754,8 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   // the small bodies' execution (walk order, 3,584 blocks) runs beside them:
   // CM 6.32-6.37 -> 6.20-6.25 ms for the two grid sizes together (A/B on one
   // box, four rounds).
-  static const u32 kBigBlocksFork = [] {  // A/B knob, separate from the one-stream launch's
-    const char* e = getenv("FSG_EXEC_BIG_BLOCKS_FORK");
-    const int v = e ? atoi(e) : 1024;
-    return v >= 1 ? (u32)v : 1024u;
-  }();
+  const i64 bbf_opt = opt(kOptExecBigBlocksFork);  // A/B knob, separate from the one-stream launch's
+  const u32 kBigBlocksFork = bbf_opt >= 1 && bbf_opt <= (1 << 20) ? (u32)bbf_opt : 1024u;
   auto launch_big = [&](hipStream_t st, const BigSet& b, u32 mode) -> hipError_t {
     hipError_t e2 = launch_index_big_set(st, b, mode);
     if (e2 != hipSuccess) return e2;
@@ -2787,15 +2769,12 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     return hipGetLastError();
   };
   // The huge messages' pass 1b, chunked (chunk_*_kernel): when the record
-  // region holds a batch of this workspace's size (FSG_CHUNKED_HUGE=0: one
-  // wave per message).  On by default since the small bodies' execution runs
+  // region holds a batch of this workspace's size (option chunked_huge 0:
+  // one wave per message).  On by default since the small bodies' execution runs
   // in walk order (FSG_SPLIT_WALK 3): CM 6.77-6.81 -> 6.44 ms, where the
   // chunked walk alone had measured slower (the huge bodies were then off
   // the critical path).
-  const bool kChunked = [] {  // (read per call: the tests run both forms)
-    const char* e = getenv("FSG_CHUNKED_HUGE");
-    return !(e && e[0] == '0');
-  }();
+  const bool kChunked = opt(kOptChunkedHuge) != 0;  // (the tests run both forms)
   const u64 max_huge = chunk_bytes / 320;
   const u64 max_recs = max_huge ? (chunk_bytes - 8 * max_huge) / sizeof(ChunkRec) : 0;
   u32* const first_rec = reinterpret_cast<u32*>(chunk_region);
@@ -2833,12 +2812,10 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   // each wave looping over messages; CM 7.31 -> 7.02 ms against one wave per
   // message (A/B on one box, two passes; 1,024 blocks: 7.11, 3,584: 7.03);
   // 3,584 (two rounds of blocks at 7 waves per SIMD) since the execution
-  // runs in walk order (see kBigBlocksFork).  FSG_SMALL_PERSIST (blocks, read
-  // per call: the tests shrink it; 0 = one wave per message).
-  const u32 kSmallPersist = [] {
-    const char* e = getenv("FSG_SMALL_PERSIST");
-    return e ? (u32)atoi(e) : 3584u;
-  }();
+  // runs in walk order (see kBigBlocksFork).  Option small_persist (blocks:
+  // the tests shrink it; 0 = one wave per message).
+  const i64 sp_opt = opt(kOptSmallPersist);
+  const u32 kSmallPersist = sp_opt >= 0 && sp_opt <= (1 << 20) ? (u32)sp_opt : 3584u;
   auto launch_small = [&](hipStream_t st, u32 part) -> hipError_t {
     // one wave per message; large ones are skipped (big_blocks = 0: no block
     // takes the large-message role).  part 1 / 2: the messages of that part
@@ -2922,13 +2899,9 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
         big_blocks, big_threshold, kPrio, keep_hist, 0u, nullptr, nullptr, 0u, 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  // Diagnostic only (FSG_DIAG_NO_TAIL=1): skip this pass to trace the
+  // Diagnostic only (option diag_no_tail 1): skip this pass to trace the
   // launch-order effect; wrong for kNeedFallback messages.
-  static const bool kNoTail = [] {
-    const char* e = getenv("FSG_DIAG_NO_TAIL");
-    return e && e[0] == '1';
-  }();
-  if (kNoTail) return hipSuccess;
+  if (opt(kOptDiagNoTail) == 1) return hipSuccess;
   fallback_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off,
                                                          out_len, status, flags);
   return hipGetLastError();

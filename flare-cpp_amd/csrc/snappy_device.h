@@ -13,6 +13,7 @@ typedef uint16_t u16;
 typedef uint32_t u32;
 typedef uint64_t u64;
 typedef int32_t i32;
+typedef int64_t i64;
 
 constexpr u32 kBlockLog = 16;                    // snappy.h:201
 constexpr u32 kBlockSize = 1u << kBlockLog;      // snappy.h:202

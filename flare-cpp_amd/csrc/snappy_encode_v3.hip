@@ -30,6 +30,7 @@
 //
 // Output bytes equal snappy::Compress(Source*, Sink*) (snappy.cc:875-954);
 // EmitLiteral / EmitCopy follow snappy.cc:156-232.
+#include "options.h"
 #include "snappy_device.h"
 
 #include <cstdlib>
@@ -628,10 +629,6 @@ EncSide* enc_side() {
   });
   return s->stream ? s : nullptr;
 }
-u32 env_u32(const char* name, u32 dflt) {
-  const char* e = getenv(name);
-  return e ? (u32)strtoul(e, nullptr, 10) : dflt;
-}
 }  // namespace
 
 hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
@@ -667,9 +664,11 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
   } else {
     wave_min = 0;
   }
-  // (read per call: the tests force the lane share with FSG_ENCODE_WAVE_ALL_MB=0)
-  const u32 kShare = env_u32("FSG_ENCODE_WAVE_SHARE", 280);  // permille
-  const u64 kAllBytes = (u64)env_u32("FSG_ENCODE_WAVE_ALL_MB", 640) << 20;
+  // (options encode_wave_share / encode_wave_all_mb: the tests force the lane
+  // share with encode_wave_all_mb 0)
+  const i64 share_opt = opt(kOptEncodeWaveShare), all_opt = opt(kOptEncodeWaveAllMb);
+  const u32 kShare = share_opt >= 0 && share_opt <= 1000 ? (u32)share_opt : 280u;  // permille
+  const u64 kAllBytes = (all_opt >= 0 && all_opt < (1 << 24) ? (u64)all_opt : 640ull) << 20;
   auto pipe = max_in_len > kBlockSize || max_in_len == 0
                   ? encode_pipe_kernel<FSG_V3_PROBES_SPLIT, FSG_V3_POST_PROBES_SPLIT>
                   : encode_pipe_kernel<kKFlat, kPostFlat>;

@@ -276,20 +276,29 @@ bool Device::run(const std::vector<Request*>& reqs, Kind kind, Counters* ctr) {
   if (!validate && slab == nullptr && !h_out.reserve(total_out + 16)) return false;
   uint8_t* hout = slab ? OutSlabData(slab) : h_out.as<uint8_t>();
 
+  // Metadata columns, back to back in this order on host and device (the
+  // one-chunk path below copies in_off..out_cap and out_len..status as two
+  // contiguous spans, so the order and the packing are load-bearing):
+  //   in_off u64[n] | out_off u64[n] | in_len u32[n] | out_cap u32[n] | out_len u32[n] | status i32[n]
+  constexpr size_t kColInOff = 0, kColOutOff = 8, kColInLen = 16, kColOutCap = 20, kColOutLen = 24, kColStatus = 28;
+  static_assert(kColOutOff == kColInOff + 8 && kColInLen == kColOutOff + 8 && kColOutCap == kColInLen + 4 &&
+                    kColOutLen == kColOutCap + 4 && kColStatus == kColOutLen + 4,
+                "the combined H2D (24n bytes from in_off) and D2H (8n bytes from out_len) copies need these "
+                "columns contiguous and in this order");
   uint8_t* m = h_meta.as<uint8_t>();
-  auto* in_off = reinterpret_cast<uint64_t*>(m);
-  auto* out_off = reinterpret_cast<uint64_t*>(m + 8ull * n);
-  auto* in_len = reinterpret_cast<uint32_t*>(m + 16ull * n);
-  auto* out_cap = reinterpret_cast<uint32_t*>(m + 20ull * n);
-  auto* out_len = reinterpret_cast<uint32_t*>(m + 24ull * n);
-  auto* status = reinterpret_cast<int32_t*>(m + 28ull * n);
+  auto* in_off = reinterpret_cast<uint64_t*>(m + kColInOff * n);
+  auto* out_off = reinterpret_cast<uint64_t*>(m + kColOutOff * n);
+  auto* in_len = reinterpret_cast<uint32_t*>(m + kColInLen * n);
+  auto* out_cap = reinterpret_cast<uint32_t*>(m + kColOutCap * n);
+  auto* out_len = reinterpret_cast<uint32_t*>(m + kColOutLen * n);
+  auto* status = reinterpret_cast<int32_t*>(m + kColStatus * n);
   uint8_t* dm = d_meta.as<uint8_t>();
-  auto* d_in_off = reinterpret_cast<uint64_t*>(dm);
-  auto* d_out_off = reinterpret_cast<uint64_t*>(dm + 8ull * n);
-  auto* d_in_len = reinterpret_cast<uint32_t*>(dm + 16ull * n);
-  auto* d_out_cap = reinterpret_cast<uint32_t*>(dm + 20ull * n);
-  auto* d_out_len = reinterpret_cast<uint32_t*>(dm + 24ull * n);
-  auto* d_status = reinterpret_cast<int32_t*>(dm + 28ull * n);
+  auto* d_in_off = reinterpret_cast<uint64_t*>(dm + kColInOff * n);
+  auto* d_out_off = reinterpret_cast<uint64_t*>(dm + kColOutOff * n);
+  auto* d_in_len = reinterpret_cast<uint32_t*>(dm + kColInLen * n);
+  auto* d_out_cap = reinterpret_cast<uint32_t*>(dm + kColOutCap * n);
+  auto* d_out_len = reinterpret_cast<uint32_t*>(dm + kColOutLen * n);
+  auto* d_status = reinterpret_cast<int32_t*>(dm + kColStatus * n);
   // pinned-block descriptors: src u64, dst offset u64, length u32 (0 = staged)
   uint8_t* g = h_gath.as<uint8_t>();
   auto* g_src = reinterpret_cast<uint64_t*>(g);

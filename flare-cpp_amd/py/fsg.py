@@ -31,6 +31,9 @@ _SIGS = {
     "fsg_last_error": (_c.c_char_p, []),
     "fsg_select_kernels": (_c.c_int, [_c.c_int, _c.c_int]),
     "fsg_set_split_region_cap": (_c.c_int, [_u32]),
+    "fsg_set_option": (_c.c_int, [_c.c_char_p, _c.c_int64]),
+    "fsg_get_option": (_c.c_int, [_c.c_char_p, _c.POINTER(_c.c_int64)]),
+    "fsg_default_option": (_c.c_int, [_c.c_char_p, _c.POINTER(_c.c_int64)]),
     "fsg_max_compressed_length": (_sz, [_sz]),
     "fsg_get_uncompressed_length": (_c.c_int, [_vp, _sz, _c.POINTER(_u32), _c.c_int]),
     "fsg_uncompressed_lengths_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _c.c_int, _vp]),
@@ -60,7 +63,8 @@ def header_symbols(header: Path | None = None) -> list[str]:
 
 
 # entry points an older library under A/B may lack
-_OPTIONAL = {"fsg_decompress_batch_2s", "fsg_lz4_decompress_batch_2s"}
+_OPTIONAL = {"fsg_decompress_batch_2s", "fsg_lz4_decompress_batch_2s", "fsg_lz4_decompress_batch_ws",
+             "fsg_lz4_decompress_workspace_bytes", "fsg_set_option", "fsg_get_option", "fsg_default_option"}
 
 
 def load_gpu_lib(path: Path | None = None) -> ctypes.CDLL:
@@ -74,6 +78,45 @@ def load_gpu_lib(path: Path | None = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
     return lib
+
+
+def get_option(name: str, lib: ctypes.CDLL | None = None) -> int:
+    """fsg_get_option: a process-wide tuning/test option (include/flare_snappy_gpu.h)."""
+    lib = lib or load_gpu_lib()
+    v = _c.c_int64(0)
+    if lib.fsg_get_option(name.encode(), _c.byref(v)) != 0:
+        raise KeyError(name)
+    return v.value
+
+
+def set_option(name: str, value: int, lib: ctypes.CDLL | None = None) -> None:
+    lib = lib or load_gpu_lib()
+    if lib.fsg_set_option(name.encode(), int(value)) != 0:
+        raise KeyError(name)
+
+
+class options:
+    """Context manager: set library options for a block, restore them after.
+
+        with fsg.options(decode_fork=1, split_walk=3): ...
+    """
+
+    def __init__(self, **kv):
+        self.kv = kv
+        self.saved = {}
+
+    def __enter__(self):
+        lib = load_gpu_lib()
+        for k, v in self.kv.items():
+            self.saved[k] = get_option(k, lib)
+            set_option(k, v, lib)
+        return self
+
+    def __exit__(self, *exc):
+        lib = load_gpu_lib()
+        for k, v in self.saved.items():
+            set_option(k, v, lib)
+        return False
 
 
 def _ptr(t) -> int | None:
@@ -156,6 +199,8 @@ class SnappyGPU:
 
     def lz4_decompress_workspace(self, n, total_in_bytes, device=None):
         import torch
+        if not hasattr(self.lib, "fsg_lz4_decompress_workspace_bytes"):
+            return None  # an older library under A/B: the one-pass kernel runs
         nbytes = self.lib.fsg_lz4_decompress_workspace_bytes(n, total_in_bytes)
         return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device or f"cuda:{self.device}")
 
@@ -165,7 +210,7 @@ class SnappyGPU:
         decoder (fsg_lz4_decompress_batch_ws; with `pass1_stream`,
         fsg_lz4_decompress_batch_2s: the index pass there, the execution on
         `stream`)."""
-        if workspace is None:
+        if workspace is None or not hasattr(self.lib, "fsg_lz4_decompress_batch_ws"):
             self._check(self.lib.fsg_lz4_decompress_batch(
                 _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_out), _ptr(d_out_off), _ptr(d_out_cap),
                 _ptr(d_out_len), _ptr(d_status), self._stream(stream)), "fsg_lz4_decompress_batch")

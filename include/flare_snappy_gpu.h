@@ -103,6 +103,24 @@ int fsg_select_kernels(int decode_variant, int encode_variant);
  * unaffected.  Process-wide. */
 int fsg_set_split_region_cap(uint32_t bytes);
 
+/* Process-wide tuning and test options (no counterpart in the reference,
+ * whose codec has no launch choices).  Each starts from its FSG_<NAME>
+ * environment variable, read once when the library is loaded; the launch
+ * paths read only this table, never the environment.  Names (values are
+ * integers; -1 = the library's automatic rule where one exists):
+ *   decode_fork (-1 | 0 | 1), split_walk (0..3), split_class, exec_keep
+ *   (bytes of history at a window slide, 512..2000, multiple of 16),
+ *   chunked_huge, small_persist, small_batch, split_huge, walk_order,
+ *   lean_walk, exec_big_blocks, exec_prio, exec_big_blocks_fork,
+ *   diag_no_tail, encode_wave_min, encode_wave_share, encode_wave_all_mb,
+ *   encode_lanes, lz4_big_min.
+ * Every value produces the same bytes and statuses.  Set between batches, not
+ * while other threads launch.  FSG_ERR_INVALID_ARG for an unknown name.
+ * fsg_default_option returns the built-in default (before the environment). */
+int fsg_set_option(const char *name, int64_t value);
+int fsg_get_option(const char *name, int64_t *value);
+int fsg_default_option(const char *name, int64_t *value);
+
 /* 32 + n + n/6 (snappy.cc:55-77). */
 size_t fsg_max_compressed_length(size_t n);
 

@@ -20,6 +20,13 @@ Outputs (all data, no code):
                  length, strict-header verdict, validator verdict
   digests_*.npz  per-message (compressed_len, fnv1a64) for the first N
                  messages of the C2/C3/CM/C5 synthetic batches
+  full_*.npz     the BASELINE configs at FULL size:
+                 per-message (input_fnv, compressed_len, compressed_fnv) of all
+                 65,536 C2 and C3 bodies, and for CM's 1,048,576 bodies the
+                 aggregate digests (fnv1a64 over the per-message fnv column,
+                 sums of lengths) plus the compressed-length column.
+                 `python tests/golden/make_golden.py --full-only` regenerates
+                 just these.
 """
 from __future__ import annotations
 
@@ -40,8 +47,55 @@ import fsg  # noqa: E402
 from gen_inputs import build_input, positive_specs, negative_cases  # noqa: E402
 
 
+def aggregate(col: np.ndarray) -> int:
+    """The checksum of checksums: fnv1a64 over a u64 digest column's bytes."""
+    a = np.ascontiguousarray(col, np.uint64)
+    return fsg.fnv1a64(a.tobytes())
+
+
+def full_digests(ref, kind, sizes, chunk=8192, threads=8):
+    """Reference compress of the whole batch (oracle/_ref, the handler's
+    Source/Sink path, `threads` host threads) in chunks of `chunk` bodies:
+    per-message input fnv, compressed length and compressed fnv."""
+    n = len(sizes)
+    in_fnv = np.zeros(n, np.uint64)
+    clen = np.zeros(n, np.uint32)
+    cfnv = np.zeros(n, np.uint64)
+    for a in range(0, n, chunk):
+        b = fsg.make_batch(kind, sizes[a:a + chunk], first_index=a)
+        caps = np.array([fsg.max_compressed_length(int(x)) for x in b.lens], np.uint64)
+        oo, tot = fsg.slot_offsets(caps)
+        out = np.zeros(tot, np.uint8)
+        ol = np.zeros(len(b), np.uint32)
+        ref.batch(0, b.data, b.offsets, b.lens, out, oo, None, ol, threads=threads)
+        in_fnv[a:a + len(b)] = fsg.digests(b.data, b.offsets, b.lens)
+        clen[a:a + len(b)] = ol
+        cfnv[a:a + len(b)] = fsg.digests(out, oo, ol)
+    return in_fnv, clen, cfnv
+
+
+def make_full(ref):
+    n = 65536
+    for name, kind, size in (("C2", fsg.KIND_RANDOM, 4096), ("C3", fsg.KIND_TEXT, 65536)):
+        in_fnv, clen, cfnv = full_digests(ref, kind, np.full(n, size, np.uint32))
+        np.savez_compressed(HERE / f"full_{name}.npz", input_fnv=in_fnv, compressed_len=clen, compressed_fnv=cfnv,
+                            aggregate=np.array([aggregate(in_fnv), aggregate(cfnv)], np.uint64))
+        print(name, "full:", n, "bodies, ratio %.3f" % (n * size / clen.sum()))
+    n = 1 << 20
+    sizes = fsg.mixed_sizes(n)
+    in_fnv, clen, cfnv = full_digests(ref, fsg.KIND_MIXED, sizes, chunk=65536)
+    np.savez_compressed(HERE / "full_CM.npz", compressed_len=clen,
+                        aggregate=np.array([aggregate(in_fnv), aggregate(cfnv)], np.uint64),
+                        totals=np.array([int(sizes.astype(np.uint64).sum()), int(clen.astype(np.uint64).sum())],
+                                        np.uint64))
+    print("CM full:", n, "bodies,", int(sizes.astype(np.uint64).sum()), "bytes")
+
+
 def main():
     ref = Reference()
+    if "--full-only" in sys.argv:
+        make_full(ref)
+        return
     vectors = []
     for spec in positive_specs():
         data = build_input(spec)
@@ -109,6 +163,7 @@ def main():
                  compressed_len=clen, compressed_fnv=cfnv)
         print(name, len(b), "bodies, ratio %.3f" % (b.total / max(1, int(clen.sum()))))
     print(len(vectors), "positive vectors,", len(neg), "negative vectors")
+    make_full(ref)
 
 
 if __name__ == "__main__":

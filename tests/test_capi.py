@@ -55,3 +55,38 @@ def test_invalid_arguments_rejected_without_gpu():
     assert rc == -1
     rc = lib.fsg_decompress_batch(None, None, None, 5, None, None, None, None, None, 0, None, 0, None)
     assert rc == -1
+
+
+def test_option_calls():
+    """fsg_set_option / fsg_get_option / fsg_default_option: known names round
+    trip, unknown names and null outputs are rejected, defaults are the
+    built-in ones (the environment is read once at load, never per call)."""
+    lib = fsg.load_gpu_lib()
+    names = ["decode_fork", "split_walk", "split_class", "exec_keep", "chunked_huge", "small_persist",
+             "small_batch", "split_huge", "walk_order", "lean_walk", "exec_big_blocks", "exec_prio",
+             "exec_big_blocks_fork", "diag_no_tail", "encode_wave_min", "encode_wave_share",
+             "encode_wave_all_mb", "encode_lanes", "lz4_big_min"]
+    v = ctypes.c_int64(0)
+    for n in names:
+        assert lib.fsg_default_option(n.encode(), ctypes.byref(v)) == 0, n
+        with fsg.options(**{n: 12345}):
+            assert fsg.get_option(n) == 12345
+        assert fsg.get_option(n) != 12345
+    assert lib.fsg_set_option(b"no_such_option", 1) == -1
+    assert lib.fsg_get_option(b"no_such_option", ctypes.byref(v)) == -1
+    assert lib.fsg_get_option(b"split_walk", None) == -1
+    assert lib.fsg_set_option(None, 1) == -1
+    assert lib.fsg_default_option(b"split_walk", ctypes.byref(v)) == 0 and v.value == 3
+    assert lib.fsg_default_option(b"decode_fork", ctypes.byref(v)) == 0 and v.value == -1
+
+
+def test_decode_launch_reads_no_environment():
+    """The drop-in's launch paths take their knobs from the option table:
+    no getenv in the HIP sources outside capi.hip's load-time read."""
+    src = Path(__file__).resolve().parents[1] / "flare-cpp_amd" / "csrc"
+    for f in src.glob("*.hip"):
+        text = f.read_text()
+        if f.name == "capi.hip":
+            assert text.count("getenv(") == 2  # env_int (kernel variants) + the option table's one-time read
+        else:
+            assert "getenv(" not in text, f.name

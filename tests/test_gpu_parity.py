@@ -66,6 +66,38 @@ def test_golden_negative_verdicts(gpu):
         assert (s == fsg.FSG_OK) == v["valid"], v["name"]
 
 
+@pytest.mark.parametrize("small_batch", [0, 64])
+def test_small_batch_verdicts(gpu, oracle, small_batch, fsg_opts):
+    """Batches of <= 64 messages index every body with a wave (pass 1b) by
+    default (option small_batch); small_batch 0 keeps them on the lane walk.
+    Both: the reference's verdicts and bytes on the negative vectors and on
+    mutated text bodies, in batches of 1, 17 and 64."""
+    fsg_opts(small_batch=small_batch)
+    negs = [v for v in json.loads((GOLDEN / "negative.json").read_text()) if v["ok"] is not None]
+    comps = [bytes.fromhex(v["hex"]) for v in negs]
+    rng = np.random.default_rng(5)
+    srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (100, 3000, 20000, 70000)]
+    for k in range(120):
+        c = bytearray(oracle.compress(srcs[k % len(srcs)]))
+        if k % 3:
+            c[int(rng.integers(len(c)))] = int(rng.integers(256))
+        if k % 7 == 0:
+            c = c[: int(rng.integers(1, len(c) + 1))]
+        comps.append(bytes(c))
+    for size in (1, 17, 64):
+        for b0 in range(0, len(comps), size if size > 1 else 11):
+            part = comps[b0:b0 + size]
+            outs, ol, st = gpu.decompress(part, [1 << 17] * len(part))
+            for c, o, s in zip(part, outs, st):
+                ok, ulen, ref = oracle.uncompress(c, cap=1 << 17)
+                if ok is None:
+                    assert s == fsg.FSG_SLOT_TOO_SMALL
+                elif not ok:
+                    assert s in (fsg.FSG_CORRUPT, fsg.FSG_BAD_HEADER)
+                else:
+                    assert s == fsg.FSG_OK and o[:ulen] == ref
+
+
 def test_strict_header_flag(gpu):
     negs = json.loads((GOLDEN / "negative.json").read_text())
     comps = [bytes.fromhex(v["hex"]) for v in negs]
@@ -125,7 +157,7 @@ def test_randomized_against_oracle(gpu, oracle, encoder):
 
 @pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1"), (0, "1p"), (0, "1s0"),
                                           (0, "1s1"), (0, "1s2")])
-def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, monkeypatch):
+def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, fsg_opts):
     """Mutated and truncated streams (64 B to 70 KB bodies).  fork "1" runs
     the path of batches over 128K messages: plan pass, the large messages'
     passes on side streams, the small ones on a persistent grid; "1p" with the small
@@ -134,9 +166,9 @@ def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, monkeypatch):
     small bodies executed in message order; 1: walk and execution split by
     size on two streams; 2: one execution launch in walk order; default 3:
     two execution launches by size)."""
-    monkeypatch.setenv("FSG_DECODE_FORK", fork[0])
-    monkeypatch.setenv("FSG_SMALL_PERSIST", "5" if fork == "1p" else "1792")
-    monkeypatch.setenv("FSG_SPLIT_WALK", fork[2] if fork.startswith("1s") else "3")
+    fsg_opts(decode_fork=fork[0])
+    fsg_opts(small_persist="5" if fork == "1p" else "1792")
+    fsg_opts(split_walk=fork[2] if fork.startswith("1s") else "3")
     gpu.codec.select_kernels(variant, 0)
     rng = np.random.default_rng(9)
     srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (64, 700, 9000, 70000)]
@@ -163,7 +195,7 @@ def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, monkeypatch):
 
 
 @pytest.mark.parametrize("fork", ["0", "1", "1c"])
-def test_large_message_index_fuzz(gpu, oracle, fork, monkeypatch):
+def test_large_message_index_fuzz(gpu, oracle, fork, fsg_opts):
     """Compressed bodies over 48 KiB take the wave-per-message index pass
     (index_big_kernel): intact, bit-flipped and truncated ones, mixed with
     small ones in one batch, against the oracle's verdicts and bytes.  With
@@ -172,8 +204,8 @@ def test_large_message_index_fuzz(gpu, oracle, fork, monkeypatch):
     default for batches of > 128K messages).  "1c": the huge bodies (> 256 KiB
     compressed) through the chunked pass 1b (FSG_CHUNKED_HUGE=1), corruption
     in every chunk position included."""
-    monkeypatch.setenv("FSG_DECODE_FORK", fork[0])
-    monkeypatch.setenv("FSG_CHUNKED_HUGE", "1" if fork == "1c" else "0")
+    fsg_opts(decode_fork=fork[0])
+    fsg_opts(chunked_huge="1" if fork == "1c" else "0")
     rng = np.random.default_rng(21)
     srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (120000, 400000, 1 << 20)]
     if fork == "1c":  # more huge bodies: 3 MiB text, text with a long random run across chunks
@@ -423,7 +455,7 @@ def _copy4(length: int, offset: int) -> bytes:
 
 
 @pytest.mark.parametrize("fork", ["0", "1", "1c"])
-def test_large_message_segments(gpu, oracle, fork, monkeypatch):
+def test_large_message_segments(gpu, oracle, fork, fsg_opts):
     """Large bodies run in pass 2 as 64 KiB output segments when no tag spans
     a segment boundary and no copy reaches below its segment (every stream the
     reference encoder writes); otherwise whole.  Raw sizes around the
@@ -431,8 +463,8 @@ def test_large_message_segments(gpu, oracle, fork, monkeypatch):
     hand-built streams that must run whole; on one stream and forked ("1c":
     the huge bodies through the chunked pass 1b, huge hand-built streams that
     must run whole included)."""
-    monkeypatch.setenv("FSG_DECODE_FORK", fork[0])
-    monkeypatch.setenv("FSG_CHUNKED_HUGE", "1" if fork == "1c" else "0")
+    fsg_opts(decode_fork=fork[0])
+    fsg_opts(chunked_huge="1" if fork == "1c" else "0")
     rng = np.random.default_rng(5)
     items = []
     for n in (65537, 131072, 131073, 131074, 131075, 131076, 196609, 300000, 1 << 20):
@@ -534,7 +566,7 @@ def test_mutations_and_trailing_tags(gpu, oracle):
 
 
 @pytest.mark.parametrize("keep", ["512", "768", "1024", "2000"])
-def test_window_slide_flush_rule(gpu, oracle, keep, monkeypatch):
+def test_window_slide_flush_rule(gpu, oracle, keep, fsg_opts):
     """A window slide must leave every byte a far piece can read in global
     memory: the piece's source lies below the new base but its 16-byte load
     reaches up to 15 bytes above it, so the slide flushes (and waits) when
@@ -545,7 +577,7 @@ def test_window_slide_flush_rule(gpu, oracle, keep, monkeypatch):
     bytes, 512 B decoded a zero at offset 343,000 of the 1 MiB golden text.
     Golden vectors (up to 1 MiB, segmented and whole), window-edge streams
     and a C3-like batch, byte-equal to the inputs."""
-    monkeypatch.setenv("FSG_EXEC_KEEP", keep)
+    fsg_opts(exec_keep=keep)
     vecs = json.loads((GOLDEN / "vectors.json").read_text())
     datas = [build_input(v) for v in vecs]
     comps = [oracle.compress(d) for d in datas]
@@ -637,20 +669,24 @@ def test_two_stream_decode_stream_of_batches(gpu, oracle):
                 assert outs[i][:ulen] == ref, (k, i)
 
 
-@pytest.mark.parametrize("fork", ["0", "1", "1p"])
+@pytest.mark.parametrize("fork", ["0", "1", "1p", "1d"])
 @pytest.mark.parametrize("fill", [0xFF, 0x5A])
-def test_decode_with_garbage_workspace(gpu, oracle, fork, fill, monkeypatch):
+def test_decode_with_garbage_workspace(gpu, oracle, fork, fill, fsg_opts):
     """The launch zeroes only the workspace's counters and lists: the index
     passes must store every bitmap word the execution pass reads (zero words,
     the words a long literal jumps over, the tail up to the allocation;
     pass 1b its whole message).  Decode with the workspace filled with
     garbage: text of many sizes, long literals inside text, single-literal
-    and large (pass 1b) bodies, intact and corrupted, against the oracle."""
-    monkeypatch.setenv("FSG_DECODE_FORK", fork[0])
-    monkeypatch.setenv("FSG_SMALL_PERSIST", "3" if fork == "1p" else "1792")
+    and large (pass 1b) bodies, a 1 MiB text body (compressed > 256 KiB: the
+    forked path's chunked huge-body walk, whose record region sits at the
+    workspace's end and is never zeroed), intact and corrupted, against the
+    oracle.  "1d": the forked path at the shipped small_persist default."""
+    fsg_opts(decode_fork=fork[0])
+    if fork != "1d":
+        fsg_opts(small_persist="3" if fork == "1p" else "1792")
     rng = np.random.default_rng(fill)
     srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0)
-            for s in (1, 33, 200, 1000, 4096, 9000, 65536, 70000, 200000)]
+            for s in (1, 33, 200, 1000, 4096, 9000, 65536, 70000, 200000, 1 << 20)]
     srcs += [fsg.make_batch(fsg.KIND_RANDOM, [s], first_index=s).item(0) for s in (100, 5000, 65536, 600000)]
     # text with random runs inside: long literals between copies
     for k in range(4):
@@ -664,10 +700,11 @@ def test_decode_with_garbage_workspace(gpu, oracle, fork, fill, monkeypatch):
         if i % 5 == 4:
             c[int(rng.integers(len(c)))] ^= 0x41
         comps.append(bytes(c))
-        caps.append(1 << 19)
+        caps.append(max(1 << 19, len(srcs[i % len(srcs)])))
+    assert max(len(c) for c in comps) > 256 * 1024
     outs, ol, st = gpu.decompress(comps, caps, ws_fill=fill)
     for i, (c, o, s) in enumerate(zip(comps, outs, st)):
-        ok, ulen, ref = oracle.uncompress(c, cap=1 << 19)
+        ok, ulen, ref = oracle.uncompress(c, cap=caps[i])
         if ok is None:
             assert s == fsg.FSG_SLOT_TOO_SMALL, i
         elif not ok:
@@ -677,7 +714,7 @@ def test_decode_with_garbage_workspace(gpu, oracle, fork, fill, monkeypatch):
 
 
 @pytest.mark.parametrize("wave_min,all_mb", [("1", "640"), ("16384", "640"), ("4096", "0")])
-def test_wave_encoder_against_oracle(gpu, oracle, wave_min, all_mb, monkeypatch):
+def test_wave_encoder_against_oracle(gpu, oracle, wave_min, all_mb, fsg_opts):
     """The wave encoder (hash table in LDS, one wave per fragment:
     csrc/snappy_encode_wave.hip) takes every fragment of a split message and
     the messages of >= FSG_ENCODE_WAVE_MIN bytes, the lane encoder the rest.
@@ -687,8 +724,8 @@ def test_wave_encoder_against_oracle(gpu, oracle, wave_min, all_mb, monkeypatch)
     the whole-message fallback) and messages of every size class.
     FSG_ENCODE_WAVE_ALL_MB=0 gives the lanes their share of the long units
     too (the split the encoder uses for batches of more than 640 MB of them)."""
-    monkeypatch.setenv("FSG_ENCODE_WAVE_MIN", wave_min)
-    monkeypatch.setenv("FSG_ENCODE_WAVE_ALL_MB", all_mb)
+    fsg_opts(encode_wave_min=wave_min)
+    fsg_opts(encode_wave_all_mb=all_mb)
     vecs = json.loads((GOLDEN / "vectors.json").read_text())
     items = [build_input(v) for v in vecs]
     rng = np.random.default_rng(int(wave_min) + 11)
@@ -752,10 +789,10 @@ def test_small_batch_wave_encoder(gpu, oracle):
 
 
 @pytest.mark.parametrize("name", ["C3", "C5"])
-def test_wave_encoder_config_digests(gpu, name, monkeypatch):
+def test_wave_encoder_config_digests(gpu, name, fsg_opts):
     """Config digests (reference-generated) with the wave encoder on every
     message of >= 16 KiB and every split fragment."""
-    monkeypatch.setenv("FSG_ENCODE_WAVE_MIN", "16384")
+    fsg_opts(encode_wave_min="16384")
     d = np.load(GOLDEN / f"digests_{name}.npz")
     n = len(d["input_len"])
     kind = {"C3": fsg.KIND_TEXT, "C5": fsg.KIND_PROTO}[name]

@@ -47,22 +47,22 @@ _WALK_MIN = {"lane_walk": "4294967295", "wave_walk": "64"}
 
 
 @pytest.fixture(params=["one_pass", "two_pass", "two_pass_lane_walk", "two_pass_wave_walk"])
-def two(request, monkeypatch):
+def two(request, fsg_opts):
     """one_pass: lz4.hip's lane kernel; two_pass: lz4_decode2.hip at its
     default thresholds (the wave walk for blocks over 64 KiB, over 2 KiB in
     batches of <= 256 messages); _lane_walk / _wave_walk force one index
     pass for every block."""
     for k, v in _WALK_MIN.items():
         if request.param.endswith(k):
-            monkeypatch.setenv("FSG_L4_BIG_MIN", v)
+            fsg_opts(lz4_big_min=v)
     return request.param != "one_pass"
 
 
 @pytest.fixture(params=["lane_walk", "wave_walk"])
-def walk(request, monkeypatch):
+def walk(request, fsg_opts):
     """The index pass of the two-pass decoder forced for every block: the
     lane walk, or (blocks of more than 64 bytes) the wave walk."""
-    monkeypatch.setenv("FSG_L4_BIG_MIN", _WALK_MIN[request.param])
+    fsg_opts(lz4_big_min=_WALK_MIN[request.param])
     return request.param
 
 
