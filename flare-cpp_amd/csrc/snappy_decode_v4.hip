@@ -1485,6 +1485,22 @@ namespace {
 #ifndef FSG_FAR_SC1
 #define FSG_FAR_SC1 1
 #endif
+#ifndef FSG_NEAR_READY_A
+#define FSG_NEAR_READY_A 1
+#endif
+// A/B knobs of the execution pass
+#ifndef FSG_SLIDE_WAIT
+#define FSG_SLIDE_WAIT 1
+#endif
+#ifndef FSG_EXEC_TAG_VALU
+#define FSG_EXEC_TAG_VALU 0
+#endif
+#ifndef FSG_ROUNDSB_OR
+#define FSG_ROUNDSB_OR 0
+#endif
+#ifndef FSG_RB_MASK
+#define FSG_RB_MASK 0
+#endif
 // Window and kept history: 3 KiB / 1 KiB at 7 waves per SIMD (C3 6.35 ->
 // 6.20 ms against 4 KiB / 2 KiB at 6 waves, A/B on one box; 4 KiB / 1 KiB
 // at 6 waves 6.33, a 256-entry tag ring 7.04).
@@ -2059,7 +2075,11 @@ __device__ __forceinline__ void exec5_message(
     // ---------- decode one tag per lane (checked by pass 1)
     const u32 s = (pos + ibal) & 3u;
     const u32 c = __builtin_amdgcn_alignbyte(pd[1], pd[0], s) & 0xffu;
+#if FSG_EXEC_TAG_VALU
+    const u32 e = exec_tag_entry(c);
+#else
     const u32 e = tagtab[c];
+#endif
     // bytes pos+1 .. pos+16 (a short literal's bytes; a copy's offset bytes)
     const bool q = s == 3;
     const u32 w0 = q ? pd[1] : pd[0], w1 = q ? pd[2] : pd[1], w2 = q ? pd[3] : pd[2];
@@ -2141,7 +2161,9 @@ __device__ __forceinline__ void exec5_message(
     if (op + tot_len - sbase > kWindow) {
       const int nsb = (int)(((op - keep_hist + obal) & ~15u)) - (int)obal;
       if ((int)flushed < nsb + 16) flush_to((u32)((int)((op + obal) & ~15u) - (int)obal));
+#if FSG_SLIDE_WAIT
       wait_all_memory();
+#endif
       const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
 #ifndef FSG_KO_SLIDE
       for (u32 k = 0; k < keep; k += 1024) {
@@ -2184,10 +2206,23 @@ __device__ __forceinline__ void exec5_message(
     const u32 nch = (len + 15) >> 4;
     const bool pat = !is_lit && off < 16 && off < len;
     // leading chunks done in round A: all of a literal's; a copy's whose
-    // 16-byte source starts below the window base (none for a pattern)
+    // 16-byte source starts below the window base (far: from the slot), then
+    // those whose source ends at or below the group's first output byte op
+    // (near-ready: final window bytes, read from LDS) -- none for a pattern.
+    // A near-ready chunk would run in the first round B anyway; in round A it
+    // is one OR store among the group's, not a read-modify-write of its own
+    // (FSG_NEAR_READY_A=0: rounds B take them, as before).
     const u32 below = (u32)(sbase - (int)src);  // > 0 as int: far
     const u32 kfar = (int)below > 0 ? ((below - 1) >> 4) + 1 : 0u;
-    const u32 kc = pat ? 0u : (kfar < nch ? kfar : nch);
+#if FSG_NEAR_READY_A
+    // chunk k's source ends at src + min(16 (k + 1), len): <= op for the
+    // first (op - src) / 16 chunks, or all of them when src + len <= op
+    const u32 kready = src + len <= op ? nch : (src < op ? (op - src) >> 4 : 0u);
+    const u32 klead = kfar > kready ? kfar : kready;
+#else
+    const u32 klead = kfar;
+#endif
+    const u32 kc = pat ? 0u : (klead < nch ? klead : nch);
     const u32 kf = fits ? (is_lit ? nch : kc) : 0u;
     const bool reg0 = is_lit && nb == 0;
     // Loads only here: the data is first used after the flush below, so all
@@ -2200,6 +2235,10 @@ __device__ __forceinline__ void exec5_message(
         const u32 a = (src + 16 * k + ibal) & ~3u;
         d = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
         d4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
+#if FSG_NEAR_READY_A
+      } else if (k >= kfar) {  // near-ready: final bytes below op in the window
+        d = lds_read16(sb + ((int)(src + 16 * k) - sbase));
+#endif
       } else {
         d = far_load(orsrc, src + 16 * k + obal);
       }
@@ -2270,18 +2309,33 @@ __device__ __forceinline__ void exec5_message(
     // loop with no per-lane pattern state (the general loop below costs ~6
     // more instructions per round).
     if (!__ballot(pat && rem > 0)) {
+#if FSG_RB_MASK
+      // the mask of the lane's last chunk, once (its other chunks are whole)
+      const u32x4 mk_last = mtab[rem ? ((rem - 1) & 15u) + 1u : 0u];
+#endif
       while (pend) {
         const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
         if (ne <= W) {
           const u32x4 x = lds_read16(sb + sw);
+#if FSG_ROUNDSB_OR
+          // OR into the zeroed window (the chunk's own bytes are still zero)
+          or_store(sb, cw, x, n, mtab);
+#else
           const u32x4 o = lds_read16(sb + cw);
+#if FSG_RB_MASK
+          const bool whole = rem > 16;
+          const u32x4 mk = u32x4{whole ? ~0u : mk_last[0], whole ? ~0u : mk_last[1], whole ? ~0u : mk_last[2],
+                                 whole ? ~0u : mk_last[3]};
+#else
           const u32x4 mk = mtab[n];
+#endif
           u32x4 y;
           y[0] = (x[0] & mk[0]) | (o[0] & ~mk[0]);
           y[1] = (x[1] & mk[1]) | (o[1] & ~mk[1]);
           y[2] = (x[2] & mk[2]) | (o[2] & ~mk[2]);
           y[3] = (x[3] & mk[3]) | (o[3] & ~mk[3]);
           __builtin_memcpy(sb + cw, &y, 16);
+#endif
           rem -= n;
           cw += n;
           sw += n;

@@ -128,8 +128,8 @@ def _ptr(t) -> int | None:
 class SnappyGPU:
     """Batched device codec through the C ABI.  Tensors must be on one cuda device."""
 
-    def __init__(self, device: int = 0):
-        self.lib = load_gpu_lib()
+    def __init__(self, device: int = 0, lib_path: Path | None = None):
+        self.lib = load_gpu_lib(lib_path)
         rc = self.lib.fsg_init(device)
         if rc != 0:
             raise RuntimeError(f"fsg_init({device}) = {rc}: {self.lib.fsg_last_error().decode()}")
