@@ -46,6 +46,10 @@
 
 namespace fsg {
 
+hipError_t launch_tiny(const u8* in, const u64* in_off, const u32* in_len, u8* out, const u64* out_off,
+                       const u32* out_len, i32* status, const u32* walk_perm, const u32* walk_hist,
+                       u32 walk_classes, u32 tiny_class, u32 blocks, hipStream_t stream);
+
 namespace {
 
 // ---- pass 1 geometry (per-lane LDS ring of input chunks, as v3)
@@ -60,6 +64,11 @@ constexpr int kIdxTagsOne = 32, kIdxTagsPlanned = 24;
 // Pass 1b walks two 64-byte windows per step (see index_big_message).
 #ifndef FSG_BIG_TWO_WINDOWS
 #define FSG_BIG_TWO_WINDOWS 1
+#endif
+// The one-stream lane walk stores its bitmap four groups at a time (see
+// index_kernel).
+#ifndef FSG_IDX_SUPER
+#define FSG_IDX_SUPER 1
 #endif
 // The tag-start bitmap is written whole by the index passes instead of
 // zeroed by the launch (see the lane walk's group stores).
@@ -238,6 +247,11 @@ __device__ __forceinline__ i32 index_prologue(
 
 // Size classes of the planned lane walk (see index_plan_kernel).
 constexpr u32 kWalkClasses = 16;
+// The tiny-body pass (snappy_decode_tiny.hip): walk classes >= kTinyClass,
+// i.e. compressed size < 2^(15 - kTinyClass + 1) = 512 B; two one-wave blocks
+// per CU (its LDS: 68.9 KB per block).
+constexpr u32 kTinyClass = 7;
+constexpr u32 kTinyBlocks = 512;
 __device__ __forceinline__ u32 walk_class(u32 n_in) {
   const u32 lg = 31u - (u32)__builtin_clz(n_in | 1u);
   return kWalkClasses - 1 - (lg < kWalkClasses - 1 ? lg : kWalkClasses - 1);
@@ -336,7 +350,16 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   // bytes the ring holds, so within 2 groups of 128 input bytes).
   constexpr int kIdxTags = kLean ? 16 : (kPlanned ? kIdxTagsPlanned : kIdxTagsOne);
   constexpr u32 kRC = kLean ? 8 : kRingChunks, kRD = kRC * 4, kAH = kLean ? 4 : kAhead;
-  constexpr u32 kBG = kLean ? 2 : 4, kBW = 4 * kBG;  // bit groups (4 words each) per lane
+  // Bit groups (4 words each) per lane.  The one-stream walk (C2, C3) stores
+  // its groups four at a time (kSuper: 64 bytes of bitmap, 512 input bytes,
+  // as four back-to-back 16-byte stores of one lane), so the L2 merges them
+  // into whole lines: stored one at a time, ~18 us apart, a lane's groups
+  // left the XCD's L2 between stores and every 16-byte store cost a line
+  // write (0.90 GB written for C3's 0.27 GB bitmap).  Its ring
+  // then holds 8 groups: the groups since the last stored super-group (<= 3)
+  // plus the <= 3 an iteration spans.  FSG_IDX_SUPER=0: one group at a time.
+  constexpr bool kSuper = FSG_IDX_SUPER && !kPlanned && !kLean;
+  constexpr u32 kBG = kLean ? 2 : (kSuper ? 8 : 4), kBW = 4 * kBG;
   // per wave, [dword][lane]; dword 64 = copy of dword 0; 65..68 absorb
   // unused prefetches
   // The lean form takes its LDS dynamically (idx_lean_lds_bytes(), given at
@@ -385,8 +408,12 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   // first one of class split_class -- the larger / the smaller bodies)
   const bool ordered = kPlanned && walk_perm;
   const u32 n_walk = ordered ? walk_hist[2 * kWalkClasses] : n_msgs;
-  const u32 split = walk_part ? walk_hist[kWalkClasses + split_class] : 0u;
-  const u32 w_lo = walk_part == 2 ? split : 0u, w_hi = walk_part == 1 ? split : n_walk;
+  // (split_class bits 8-15, when set: the first class the tiny-body pass
+  // takes -- positions from its first one are not walked here)
+  const u32 tcls = split_class >> 8;
+  const u32 split = walk_part ? walk_hist[kWalkClasses + (split_class & 0xffu)] : 0u;
+  const u32 t_hi = tcls ? walk_hist[kWalkClasses + tcls] : n_walk;
+  const u32 w_lo = walk_part == 2 ? split : 0u, w_hi = walk_part == 1 ? split : t_hi;
   const bool valid_msg = ordered ? gid < w_hi - w_lo : gid < n_walk;
   const u32 m = ordered ? (valid_msg ? walk_perm[w_lo + gid] : 0u) : gid;
 
@@ -567,22 +594,50 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     // remaining groups up to the allocation (ceil(n_in / 128)).
     if (bm && !single_src) {
       const u32 ngroups = (((n_in + 31) >> 5) + 3) >> 2;
-      const u32 cur = status < 0 ? ip >> 7 : (status == kOk ? ngroups : 0u);
+      const u32 cur0 = status < 0 ? ip >> 7 : (status == kOk ? ngroups : 0u);
+      // super-group stores: while walking, only the whole super-groups below
+      // the current one; once the walk is over, everything up to the end
+      const u32 cur = kSuper && status < 0 ? cur0 & ~3u : cur0;
+      if constexpr (kSuper) {
+        // fg is a multiple of 4 until the walk ends: the super-group at fg
+        // is one half of the 8-slot ring; past fg + 4 only after a long
+        // literal (or at the end)
+        auto super_store = [&](u32 g0) {
+          const u32 sl = (g0 & 4u) * 4;
+          u32x4 v[4];
 #pragma unroll
-      for (u32 k = 0; k < kBG; ++k) {
-        const u32 gi = fg + k;
-        if (gi < cur) {
-          const u32 sl = (gi & (kBG - 1)) * 4;
-          u32x4 v;
+          for (u32 q = 0; q < 16; ++q) v[q >> 2][q & 3] = bmr[(sl + q) * kWave + lane];
 #pragma unroll
-          for (u32 q = 0; q < 4; ++q) v[q] = bmr[(sl + q) * kWave + lane];
-          *reinterpret_cast<u32x4*>(bm + 4 * gi) = v;
+          for (u32 k = 0; k < 4; ++k)
+            if (g0 + k < cur) *reinterpret_cast<u32x4*>(bm + 4 * (g0 + k)) = v[k];
 #pragma unroll
-          for (u32 q = 0; q < 4; ++q) bmr[(sl + q) * kWave + lane] = 0;
+          for (u32 q = 0; q < 16; ++q) bmr[(sl + q) * kWave + lane] = 0;
+        };
+        if (cur > fg) {
+          super_store(fg);
+          if (cur > fg + 4) {
+            super_store(fg + 4);
+            for (u32 gi = fg + 8; gi < cur; ++gi) *reinterpret_cast<u32x4*>(bm + 4 * gi) = u32x4{0, 0, 0, 0};
+          }
+          fg = cur;
         }
+      } else {
+#pragma unroll
+        for (u32 k = 0; k < kBG; ++k) {
+          const u32 gi = fg + k;
+          if (gi < cur) {
+            const u32 sl = (gi & (kBG - 1)) * 4;
+            u32x4 v;
+#pragma unroll
+            for (u32 q = 0; q < 4; ++q) v[q] = bmr[(sl + q) * kWave + lane];
+            *reinterpret_cast<u32x4*>(bm + 4 * gi) = v;
+#pragma unroll
+            for (u32 q = 0; q < 4; ++q) bmr[(sl + q) * kWave + lane] = 0;
+          }
+        }
+        for (u32 gi = fg + kBG; gi < cur; ++gi) *reinterpret_cast<u32x4*>(bm + 4 * gi) = u32x4{0, 0, 0, 0};
+        fg = cur > fg ? cur : fg;
       }
-      for (u32 gi = fg + kBG; gi < cur; ++gi) *reinterpret_cast<u32x4*>(bm + 4 * gi) = u32x4{0, 0, 0, 0};
-      fg = cur > fg ? cur : fg;
     }
 #else
     if (bm) {
@@ -1501,6 +1556,12 @@ namespace {
 #ifndef FSG_RB_MASK
 #define FSG_RB_MASK 0
 #endif
+#ifndef FSG_FILL_PAIRS
+#define FSG_FILL_PAIRS 0
+#endif
+#ifndef FSG_PF_POS
+#define FSG_PF_POS 0
+#endif
 // Window and kept history: 3 KiB / 1 KiB at 7 waves per SIMD (C3 6.35 ->
 // 6.20 ms against 4 KiB / 2 KiB at 6 waves, A/B on one box; 4 KiB / 1 KiB
 // at 6 waves 6.33, a 256-entry tag ring 7.04).
@@ -2014,6 +2075,7 @@ __device__ __forceinline__ void exec5_message(
   u32 bmw = fill_word(scan);
   // the next group's tag bytes: 20 bytes from the dword below the tag
   u32 pf_head = 0xffffffffu, pf_cnt = 0;
+  u32 pf_pos = 0;  // the ring positions the prefetch used (FSG_PF_POS)
   u32x4 pd = u32x4{0, 0, 0, 0};
   u32 pd4 = 0;
   auto prefetch = [&](u32 p) {
@@ -2049,12 +2111,40 @@ __device__ __forceinline__ void exec5_message(
       if (bitbase < ip0) bits &= bitbase + 8 <= ip0 ? 0u : (0xffu << (ip0 - bitbase)) & 0xffu;
       const u32 cnt = __builtin_popcount(bits);
       const u32 incl = dpp_incl_scan(cnt);
+#if FSG_FILL_PAIRS
+      // Two positions per iteration, a lane's bits from the highest down:
+      // with an odd count the first pair's second dword (one past the lane's
+      // last slot) is garbage, which lands on the next lane's first slot (or
+      // past the tail) BEFORE that lane writes it -- its lowest slot is
+      // written in its last pair's first-position store, at this iteration or
+      // later, after every lane's second-position store of the iteration.
+      u32 rem = cnt;
+      const u32 a0 = tail + incl - cnt;
+      while (rem) {
+        const u32 h = 31u - __builtin_clz(bits);
+        const u32 b1 = bits & ~(1u << h);
+        const u32 h2 = b1 ? 31u - __builtin_clz(b1) : 0u;
+        const bool odd = rem & 1u;
+        const u32 at = a0 + rem - (odd ? 1u : 2u);
+        u32* const r0 = ring + (at & (kTagRing - 1));
+        u32* const r1 = ring + ((at + 1) & (kTagRing - 1));
+        // (two stores: the garbage dword first, so the next lane's own store
+        // of that slot -- in this iteration's second store at the latest --
+        // lands after it)
+        *r1 = bitbase + h;
+        wave_lds_fence();
+        *r0 = bitbase + (odd ? h : h2);
+        bits = odd ? b1 : (b1 & ~(1u << h2));
+        rem -= odd ? 1u : 2u;
+      }
+#else
       u32 slot = tail + incl - cnt;
       while (bits) {
         ring[slot & (kTagRing - 1)] = bitbase + __builtin_ctz(bits);
         ++slot;
         bits &= bits - 1;
       }
+#endif
       tail += readlane(incl, 63);
       scan += kFillWords;
       bmw = fill_word(scan);
@@ -2068,8 +2158,18 @@ __device__ __forceinline__ void exec5_message(
     const bool valid = lane < take0;
     // every lane reads the ring and prefetches: a lane past the valid tags
     // reads a stale position, whose buffer loads return message bytes or 0
+#if FSG_PF_POS
+    // the prefetch's ring positions are this group's unless a fill added
+    // tags after it: then read the ring and prefetch again
+    u32 pos = pf_pos;
+    if (pf_head != head || pf_cnt < take0) {
+      pos = ring[(head + lane) & (kTagRing - 1)];
+      prefetch(pos);
+    }
+#else
     const u32 pos = ring[(head + lane) & (kTagRing - 1)];
     if (pf_head != head || pf_cnt < take0) prefetch(pos);
+#endif
     if (prio) __builtin_amdgcn_s_setprio(1);
 
     // ---------- decode one tag per lane (checked by pass 1)
@@ -2185,7 +2285,8 @@ __device__ __forceinline__ void exec5_message(
       const u32 nh = head + k_tags;
       const u32 na = tail - nh;
       const u32 ncnt = na < 64 ? na : 64u;
-      prefetch(ring[(nh + lane) & (kTagRing - 1)]);
+      pf_pos = ring[(nh + lane) & (kTagRing - 1)];
+      prefetch(pf_pos);
       pf_head = nh;
       pf_cnt = ncnt;
     }
@@ -2450,8 +2551,12 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
       // the messages in walk order (forked path): positions [lo, hi) of
       // walk_perm -- part 1 / 2 the larger / smaller bodies, 3 all of them
       const u32 n_walk = walk_hist[2 * kWalkClasses];
-      const u32 split = walk_hist[kWalkClasses + split_class];
-      const u32 lo = walk_part == 2 ? split : 0u, hi = walk_part == 1 ? split : n_walk;
+      // (split_class bits 8-15: the tiny-body pass's first class, whose
+      // positions on are not executed here)
+      const u32 tcls = split_class >> 8;
+      const u32 split = walk_hist[kWalkClasses + (split_class & 0xffu)];
+      const u32 t_hi = tcls ? walk_hist[kWalkClasses + tcls] : n_walk;
+      const u32 lo = walk_part == 2 ? split : 0u, hi = walk_part == 1 ? split : t_hi;
       for (u32 i = m0; i < hi - lo; i = i + step < i ? 0xffffffffu : i + step) {
         const u32 m = walk_perm[lo + i];
         run(m, ring, pmap, sb, lane, status[m], 0u, 0u, out_len[m]);
@@ -2733,12 +2838,17 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   const u32 split_mode = (u32)opt(kOptSplitWalk);
   const bool split_walk = split_mode == 1;
   const u32 kSplitClass = (u32)opt(kOptSplitClass) % kWalkClasses;
+  // The tiny-body pass (snappy_decode_tiny.hip): walk classes >= kTinyClass
+  // (compressed < 512 B) decoded one body per lane in LDS, in mode 3 only;
+  // the lane walk and the small bodies' execution stop at its first class.
+  const bool tiny = opt(kOptTinyPass) != 0 && split_mode == 3 && kSplitClass < kTinyClass;
+  const u32 tiny_bits = tiny ? kTinyClass << 8 : 0u;
   auto launch_index = [&](bool planned, hipStream_t st = nullptr, u32 part = 0) -> hipError_t {
     if (planned)
       index_kernel<true><<<idx_blocks, 64 * kIdxWaves, 0, st ? st : stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
           cap_words, big_count, big_list, big_threshold, kWalkOrder ? walk_perm : nullptr, walk_hist, part,
-          kSplitClass);
+          kSplitClass | tiny_bits);
     else if (two && kLeanWalk)
       index_kernel<false, true><<<idx_blocks, 64 * kIdxWaves, idx_lean_lds_bytes(), stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
@@ -2879,7 +2989,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), set0.seg_count, whole_list, set0.whole_count, set0.exec_next,
         0u, big_threshold, 0u, keep_hist, grid < small_blocks ? grid : 0u, part ? walk_perm : nullptr,
-        part ? walk_hist : nullptr, part, kSplitClass);
+        part ? walk_hist : nullptr, part, kSplitClass | tiny_bits);
     return hipGetLastError();
   };
   SideStream* side = fork ? side_stream() : nullptr;
@@ -2923,6 +3033,12 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
       if ((e = launch_small(stream, 2u)) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(stream, side->join3, 0)) != hipSuccess) return e;
     } else {
+      if (tiny && kWalkOrder) {
+        // the tiny bodies first: one lane each, the walk skips them
+        if ((e = launch_tiny(in, in_off, in_len, out, out_off, out_len, status, walk_perm, walk_hist,
+                             kWalkClasses, kTinyClass, kTinyBlocks, stream)) != hipSuccess)
+          return e;
+      }
       if ((e = launch_index(true)) != hipSuccess) return e;
       if (kWalkOrder && split_mode == 2) {
         if ((e = launch_small(stream, 3u)) != hipSuccess) return e;

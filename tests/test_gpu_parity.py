@@ -156,7 +156,7 @@ def test_randomized_against_oracle(gpu, oracle, encoder):
 
 
 @pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1"), (0, "1p"), (0, "1s0"),
-                                          (0, "1s1"), (0, "1s2")])
+                                          (0, "1s1"), (0, "1s2"), (0, "1t0")])
 def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, fsg_opts):
     """Mutated and truncated streams (64 B to 70 KB bodies).  fork "1" runs
     the path of batches over 128K messages: plan pass, the large messages'
@@ -165,8 +165,10 @@ def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, fsg_opts):
     ~150 messages (FSG_SMALL_PERSIST); "1sK" with FSG_SPLIT_WALK=K (0: the
     small bodies executed in message order; 1: walk and execution split by
     size on two streams; 2: one execution launch in walk order; default 3:
-    two execution launches by size)."""
+    two execution launches by size; bodies under 512 compressed bytes one per
+    lane by the tiny-body pass, "1t0" without it)."""
     fsg_opts(decode_fork=fork[0])
+    fsg_opts(tiny_pass=0 if fork == "1t0" else 1)
     fsg_opts(small_persist="5" if fork == "1p" else "1792")
     fsg_opts(split_walk=fork[2] if fork.startswith("1s") else "3")
     gpu.codec.select_kernels(variant, 0)
@@ -337,6 +339,59 @@ def test_pattern_copies_and_ring_jumps(gpu, oracle, variant):
             assert s == fsg.FSG_OK and o == raw, i
     finally:
         gpu.codec.select_kernels(0, 0)
+
+
+@pytest.mark.parametrize("tiny", [1, 0])
+def test_tiny_body_pass(gpu, oracle, tiny, fsg_opts):
+    """Bodies under 512 compressed bytes on the forked path go through the
+    tiny-body pass (snappy_decode_tiny.hip: one lane per body, output in LDS):
+    text of every small size, hand-built streams (patterns of every offset,
+    COPY_4, 4-byte literal lengths, literals over 64 bytes from global memory),
+    random single literals, runs whose output exceeds the pass's 768 bytes
+    (the serial fallback), the reference's negative vectors and mutated
+    bodies, trailing zero-length literals -- bytes and statuses against the
+    oracle.  tiny=0: the same batch through the lane walk + execution."""
+    fsg_opts(decode_fork=1, tiny_pass=tiny)
+    rng = np.random.default_rng(77 + tiny)
+    comps = []
+    for n in list(range(1, 200, 7)) + list(range(200, 800, 23)):
+        comps.append(oracle.compress(fsg.make_batch(fsg.KIND_TEXT, [n], first_index=n).item(0)))
+    for i in range(400):
+        c, _ = _synthetic_stream(rng, int(rng.integers(1, 760)))
+        comps.append(c)
+    for n in (1, 15, 16, 17, 63, 64, 65, 100, 300, 490):
+        comps.append(oracle.compress(rng.integers(0, 256, n, dtype=np.uint8).tobytes()))
+    for n in (700, 768, 769, 2000, 5000, 20000):  # runs: small compressed, large output
+        comps.append(oracle.compress(bytes([n % 251]) * n))
+    comps.append(b"\x05" + _lit(b"abcde"))                          # 1-byte literal length field
+    comps.append(b"\x46" + b"\xf0\x45" + bytes(range(70)))           # literal of 70 bytes, nb = 1
+    comps.append(b"\x46" + b"\xfc\x45\x00\x00\x00" + bytes(range(70)))  # nb = 4
+    comps.append(b"\x0a" + _lit(b"ab") + _copy(2, 8, wide=True))
+    base = list(comps)
+    for _ in range(600):
+        c = bytearray(base[int(rng.integers(len(base)))])
+        for _ in range(int(rng.integers(1, 3))):
+            c[int(rng.integers(len(c)))] = int(rng.integers(256))
+        if rng.random() < 0.2:
+            c = c[: int(rng.integers(1, len(c) + 1))]
+        comps.append(bytes(c))
+    comps += [c + b"\xfc\xff\xff\xff\xff" for c in base[:40]]
+    comps += [bytes.fromhex(v["hex"]) for v in json.loads((GOLDEN / "negative.json").read_text())
+              if v["header_ok"] and v["ulen"] <= 1 << 16]
+    # padded with larger text bodies so the batch has every path of the fork
+    comps += [oracle.compress(fsg.make_batch(fsg.KIND_TEXT, [n], first_index=n).item(0))
+              for n in (3000, 9000, 70000)]
+    assert sum(len(c) < 512 for c in comps) > 1000
+    caps = [1 << 17] * len(comps)
+    outs, ol, st = gpu.decompress(comps, caps)
+    for i, (c, o, s) in enumerate(zip(comps, outs, st)):
+        ok, ulen, ref = oracle.uncompress(c, cap=caps[i])
+        if ok is None:
+            assert s == fsg.FSG_SLOT_TOO_SMALL, i
+        elif not ok:
+            assert s in (fsg.FSG_CORRUPT, fsg.FSG_BAD_HEADER), (i, c[:16].hex(), s)
+        else:
+            assert s == fsg.FSG_OK and o[:ulen] == ref, (i, c[:16].hex(), s)
 
 
 @pytest.mark.parametrize("total_in", [0, 1, 4096, 60000])
