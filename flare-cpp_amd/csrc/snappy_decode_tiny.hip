@@ -29,6 +29,15 @@
 // the execution pass touch.  A body of more than kTinyOut output bytes in
 // those classes (possible only for ratios above 1.5) gets kNeedFallback: the
 // final pass decodes it serially (fallback_kernel).
+//
+// MEASURED SLOWER, off by default (option tiny_pass):
+// CM 6.2 -> 7.5 ms (per-lane contiguous LDS) / 8.0 ms (this dword-interleaved
+// form).  The pass took 2.5 / 4.7 ms for the 595K bodies the lane walk and
+// execution pass handle in ~2.3 ms: its LDS allows two waves per CU, each
+// lane's tag loop is a chain of dependent LDS round trips with divergent
+// literal / copy / pattern paths, and while it runs the side streams' passes
+// find no LDS.  Kept, tested (test_tiny_body_pass, the "1t1" fuzz mode), as
+// the measured alternative.
 #include "snappy_lane_decode.h"
 #include "snappy_pieces.h"
 #include "wave_util.h"
@@ -36,12 +45,12 @@
 namespace fsg {
 
 namespace {
-constexpr u32 kTinyOut = 768;                       // output bytes a lane holds
-constexpr u32 kTinyOutCap = kTinyOut + 16;          // + the over-copy tail
-constexpr u32 kTinyRingChunks = 16;                 // 16-byte input chunks in the ring
-constexpr u32 kTinyRing = 16 * kTinyRingChunks;     // 256 B
-constexpr u32 kTinyLane = kTinyOutCap + kTinyRing + 16;  // + a mirror of slot 0: 1,056 B
-constexpr u32 kTinyLongLit = 64;                    // longer literals come from global memory
+constexpr u32 kTinyOut = 768;            // output bytes a lane holds
+constexpr u32 kTinyOutDw = 200;          // dwords of output per lane (+ the over-write tail, <= 19 B)
+constexpr u32 kTinyRingDw = 64;          // dwords of input ring per lane (256 B, 16 chunks)
+constexpr u32 kTinyRingChunks = kTinyRingDw / 4;
+constexpr u32 kTinySync = 8;             // tag steps between the wave's ring landings
+static_assert(kTinyOutDw * 4 >= kTinyOut + 20, "over-write tail");
 
 // The tag table of exec5_message (exec_tag_entry, snappy_decode_v4.hip): per
 // tag byte c, bits 0-4 the right shift of 0xffffffff masking the nb extra
@@ -66,21 +75,21 @@ __device__ __forceinline__ u32 tiny_tag_entry(u32 c) {
   }
   return ((32 - 8 * nb) & 31) | (ll << 5) | (lit << 6) | (len << 8) | (nb << 16) | (hi << 20);
 }
-
-__device__ __forceinline__ u32x4 lds16(const u8* p) {
-  u32x4 v;
-  __builtin_memcpy(&v, p, 16);
-  return v;
-}
-__device__ __forceinline__ void sts16(u8* p, u32x4 v) { __builtin_memcpy(p, &v, 16); }
 }  // namespace
 
-// One wave per block; kTinyBlocksPerCU blocks fill a CU's LDS.
+// The lane's LDS is dword-interleaved ([dword][lane]: dword d of lane l at
+// d * 64 + l), so a wave's dword accesses at per-lane offsets never share a
+// bank; a 16-byte read at any byte offset is five dword reads and a byte
+// shift, a 16-byte write five dword writes (the first merged with the bytes
+// below it) -- against one LDS cycle per lane for an unaligned 16-byte read
+// and two for a write in a per-lane contiguous layout ("LDS
+// access costs").  One wave per block; two blocks fill a CU's LDS.
 __global__ __launch_bounds__(64) void tiny_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u8* out,
     const u64* __restrict__ out_off, const u32* __restrict__ out_len, i32* __restrict__ status,
     const u32* __restrict__ walk_perm, const u32* __restrict__ walk_hist, u32 walk_classes, u32 tiny_class) {
-  __shared__ __attribute__((aligned(16))) u8 lds[64 * kTinyLane];
+  __shared__ u32 outs[kTinyOutDw * 64];
+  __shared__ u32 rings[kTinyRingDw * 64];
   __shared__ u32 tagtab[256];
   __shared__ u32x4 sel_tab[16];
   const u32 lane = threadIdx.x;
@@ -88,8 +97,36 @@ __global__ __launch_bounds__(64) void tiny_kernel(
   for (u32 q = 0; q < 4; ++q) tagtab[4 * lane + q] = tiny_tag_entry(4 * lane + q);
   init_pattern_table(sel_tab, lane);
   __syncthreads();
-  u8* const ol = lds + lane * kTinyLane;  // output [0, kTinyOutCap)
-  u8* const rg = ol + kTinyOutCap;        // ring [0, 256) + mirror of [0, 16) at 256
+  u32* const ol = outs + lane;   // dword d at ol[64 d]
+  u32* const rl = rings + lane;  // dword d at rl[64 (d & 63)]
+
+  // 16 bytes at byte b of the output (o) or the ring (r)
+  auto read16 = [&](bool ring, u32 b) -> u32x4 {
+    const u32 d = b >> 2, sh = b & 3;
+    u32 w[5];
+#pragma unroll
+    for (u32 q = 0; q < 5; ++q) w[q] = ring ? rl[64 * ((d + q) & (kTinyRingDw - 1))] : ol[64 * (d + q)];
+    return u32x4{__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
+                 __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh)};
+  };
+  // x to output bytes [o, o + 16); the bytes of the first dword below o are
+  // kept, up to 3 bytes past o + 16 are overwritten (later tags rewrite them)
+  auto write16 = [&](u32 o, u32x4 x) {
+    const u32 d = o >> 2, sh = o & 3;
+    if (sh == 0) {
+#pragma unroll
+      for (u32 q = 0; q < 4; ++q) ol[64 * (d + q)] = x[q];
+    } else {
+      const u32 old = ol[64 * d];
+      const u32 keep = 0xffffffffu >> (32 - 8 * sh);
+      const u32 r = 4 - sh;
+      ol[64 * d] = (old & keep) | (x[0] << (8 * sh));
+      ol[64 * (d + 1)] = __builtin_amdgcn_alignbyte(x[1], x[0], r);
+      ol[64 * (d + 2)] = __builtin_amdgcn_alignbyte(x[2], x[1], r);
+      ol[64 * (d + 3)] = __builtin_amdgcn_alignbyte(x[3], x[2], r);
+      ol[64 * (d + 4)] = x[3] >> (8 * r);
+    }
+  };
 
   const u32 lo = walk_hist[walk_classes + tiny_class];
   const u32 hi = walk_hist[2 * walk_classes];
@@ -111,8 +148,8 @@ __global__ __launch_bounds__(64) void tiny_kernel(
       status[m] = kNeedFallback;
       act = false;
     }
-    // the ring's first 16 chunks, landed now, and the next 8 in flight
-    // (chunks past the body read 0)
+    // the ring's 16 chunks, landed now, and the next 8 in flight (chunks
+    // past the body read 0)
     u32x4 g[kTinyRingChunks];
 #pragma unroll
     for (u32 k = 0; k < kTinyRingChunks; ++k) g[k] = __builtin_amdgcn_raw_buffer_load_b128(irsrc, 16 * k, 0, 0);
@@ -120,50 +157,67 @@ __global__ __launch_bounds__(64) void tiny_kernel(
 #pragma unroll
     for (u32 k = 0; k < 8; ++k) h[k] = __builtin_amdgcn_raw_buffer_load_b128(irsrc, 16 * (kTinyRingChunks + k), 0, 0);
 #pragma unroll
-    for (u32 k = 0; k < kTinyRingChunks; ++k) sts16(rg + 16 * k, g[k]);
-    sts16(rg + kTinyRing, g[0]);
+    for (u32 k = 0; k < kTinyRingChunks; ++k)
+#pragma unroll
+      for (u32 q = 0; q < 4; ++q) rl[64 * (4 * k + q)] = g[k][q];
     u32 wend = kTinyRingChunks;  // chunks [wend - 16, wend) are in the ring, [wend, wend + 8) in h
     // header length (checked by the plan pass: <= 5 bytes, < 0x80 ends it)
     u32 ip = 0;
     {
-      const u32x4 hv = lds16(rg + ibal);
-      const u64 hb = (u64)hv[0] | ((u64)hv[1] << 32);
+      const u32x4 hr = read16(true, ibal);
+      const u64 hb = (u64)hr[0] | ((u64)hr[1] << 32);
       u32 k = 0;
       while (k < 4 && ((hb >> (8 * k)) & 0x80u)) ++k;
       ip = k + 1;
     }
     u32 op = 0;
     i32 st = kOk;
-    while (__any(act)) {
-      if (act) {
-        // ---- one tag (bounds and the writer's checks as the two-pass decoder)
-        const u32 P = ip + ibal;
-        // The tag's <= 5 bytes (and a short literal's bytes) must be in the
-        // ring, else the prefetched chunks land and the tag runs next time.
-        // A landing never overwrites an unread chunk: a tag spans at most 66
-        // bytes (6 chunks), so it needs a chunk >= wend only when wend <= pc + 5,
-        // and the 8 chunks landed (< pc + 16) take the slots of chunks < pc.
-        auto land = [&]() {
+    u32 lrem = 0;  // bytes of a literal still to copy (longer than the ring holds)
+    // Landings are wave-wide, every kTinySync tag steps: a lane whose next
+    // bytes are not in the ring idles until then, so no lane's wait for its
+    // input stalls the others (a wave's loads and stores share one counter:
+    // any wait inside the loop would wait for every load issued before it).
+    // The chunks landed were requested one landing earlier; the output and
+    // the statuses are stored after the round, when every lane is done.
+    for (u32 it = 0; __any(act); ++it) {
+      if ((it & (kTinySync - 1)) == kTinySync - 1) {
+        // land h where its 8 slots hold consumed chunks only (those below
+        // the chunk of the next byte the lane reads), then request the next 8
+        const u32 pc = (ip + ibal) >> 4;
+        if (act && wend + 8 <= pc + kTinyRingChunks) {
 #pragma unroll
-          for (u32 k = 0; k < 8; ++k) {
-            const u32 sl = (wend + k) & (kTinyRingChunks - 1);
-            sts16(rg + 16 * sl, h[k]);
-            if (sl == 0) sts16(rg + kTinyRing, h[k]);
-          }
+          for (u32 k = 0; k < 8; ++k)
+#pragma unroll
+            for (u32 q = 0; q < 4; ++q) rl[64 * ((4 * (wend + k) + q) & (kTinyRingDw - 1))] = h[k][q];
           wend += 8;
 #pragma unroll
           for (u32 k = 0; k < 8; ++k) h[k] = __builtin_amdgcn_raw_buffer_load_b128(irsrc, 16 * (wend + k), 0, 0);
-        };
-        if (ip == n_in) {  // end of input between tags (:858-868), empty bodies included
+        }
+      }
+      if (act) {
+        const u32 P = ip + ibal;
+        const u32 have_end = 16 * wend;  // ring bytes end (aligned-buffer offset)
+        // this step's piece source (ring / output), its length and the
+        // number of 16-byte (or pattern-step) pieces
+        bool from_ring = true, pattern = false;
+        u32 src = 0, cnt = 0, stp = 16, off = 0;
+        if (lrem) {
+          // ---- more of a long literal, as far as the ring holds it
+          const u32 avail = have_end - P;
+          cnt = lrem < avail ? lrem : (avail & ~15u);
+          src = P;
+          lrem -= cnt;
+          ip += cnt;
+        } else if (ip == n_in) {  // end of input between tags (:858-868), empty bodies included
           st = op == ulen ? kOk : kCorrupt;
           act = false;
-        } else if (((P + 4) >> 4) >= wend) {
-          land();
-        } else {
-          const u32x4 tv = lds16(rg + (P & (kTinyRing - 1)));
-          const u32 c = tv[0] & 0xffu;
-          const u32 e = tagtab[c];
-          const u32 ext = __builtin_amdgcn_alignbyte(tv[1], tv[0], 1);
+        } else if (P + 5 <= have_end || ibal + n_in <= have_end) {
+          // ---- one tag (bounds and the writer's checks as the two-pass decoder)
+          const u32 d = P >> 2, bs = P & 3;
+          const u32 w0 = rl[64 * (d & (kTinyRingDw - 1))], w1 = rl[64 * ((d + 1) & (kTinyRingDw - 1))];
+          const u32 t0 = __builtin_amdgcn_alignbyte(w1, w0, bs);
+          const u32 ext = __builtin_amdgcn_alignbyte(w1 >> (8 * bs), t0, 1);
+          const u32 e = tagtab[t0 & 0xffu];
           const u32 val = ext & (0xffffffffu >> (e & 31u));
           const bool is_lit = e & 64u;
           const u32 nb = (e >> 16) & 7u;
@@ -176,57 +230,63 @@ __global__ __launch_bounds__(64) void tiny_kernel(
           if (step > n_in - ip || step < adv) {  // runs past the input (or wraps)
             st = kCorrupt;
             act = false;
-          } else if (is_lit && len <= kTinyLongLit && ((P + step - 1) >> 4) >= wend) {
-            land();
           } else if (len > ulen - op) {  // writer overrun (:1166, :1400)
             st = kCorrupt;
             act = false;
           } else if (is_lit) {
-            const u32 S = P + 1 + nb;  // the literal's bytes, aligned-buffer offset
-            if (len <= kTinyLongLit) {
-              for (u32 k = 0; k < len; k += 16) sts16(ol + op + k, lds16(rg + ((S + k) & (kTinyRing - 1))));
-            } else {
-              for (u32 k = 0; k < len; k += 16) sts16(ol + op + k, rsrc_load16(irsrc, S + k));
-            }
-            op += len;
-            ip += step;
+            // the tag, then as many whole 16-byte pieces of the literal as
+            // the ring holds (all of it when it ends there): the rest later
+            const u32 S = P + 1 + nb;
+            const u32 avail = have_end - S;
+            cnt = len <= avail ? len : (avail & ~15u);
+            src = S;
+            ip += 1 + nb + cnt;
+            lrem = len - cnt;
           } else {
-            const u32 off = val + (e >> 20);
+            off = val + (e >> 20);
             if (off == 0 || off > op) {  // (:1200, :1410, :1466)
               st = kCorrupt;
               act = false;
             } else {
-              const u8* src = ol + op - off;
-              if (off >= 16) {
-                for (u32 k = 0; k < len; k += 16) sts16(ol + op + k, lds16(src + k));
-              } else {
-                const u32x4 x = expand_pattern(lds16(src), off, sel_tab);
-                const u32 stp = pat_step(off);
-                for (u32 k = 0; k < len; k += stp) sts16(ol + op + k, x);
-              }
-              op += len;
+              from_ring = false;
+              src = op - off;
+              cnt = len;
+              pattern = off < 16;
+              stp = pattern ? pat_step(off) : 16u;
               ip += step;
             }
           }
         }
-        if (act && ip == n_in) {  // (the same test, one iteration sooner)
-          st = op == ulen ? kOk : kCorrupt;
-          act = false;
-        }
-        if (!act) {  // this lane's body is done: its status, and its bytes
-          status[m] = st;
-          if (st == kOk) {
-            u8* ob = out + out_off[m];
-            for (u32 k = 0; k < ulen; k += 16) store_exact(ob + k, lds16(ol + k), ulen - k < 16 ? ulen - k : 16u);
+        // ---- the pieces: cnt bytes from src to op (a pattern: one 16-byte
+        // expansion, stp bytes per piece)
+        u32x4 x = u32x4{0, 0, 0, 0};
+        for (u32 k = 0; k < cnt; k += stp) {
+          if (k == 0 || !pattern) {
+            x = read16(from_ring, src + k);
+            if (pattern) x = expand_pattern(x, off, sel_tab);
           }
+          write16(op + k, x);
         }
+        op += cnt;
       }
       wave_lds_fence();
     }
+    // ---- the round's bodies and statuses
+    if (have && status[m] == kNeedLaneWalk) {
+      status[m] = st;
+      if (st == kOk) {
+        u8* ob = out + out_off[m];
+        for (u32 k = 0; k < ulen; k += 16) {
+          const u32x4 v = u32x4{ol[64 * (k / 4)], ol[64 * (k / 4 + 1)], ol[64 * (k / 4 + 2)], ol[64 * (k / 4 + 3)]};
+          store_exact(ob + k, v, ulen - k < 16 ? ulen - k : 16u);
+        }
+      }
+    }
+    wave_lds_fence();
   }
 }
 
-// Grid: two one-wave blocks per CU (kTinyLane x 64 + tables = 68.9 KB each).
+// Grid: two one-wave blocks per CU (68.5 KB of LDS each).
 hipError_t launch_tiny(const u8* in, const u64* in_off, const u32* in_len, u8* out, const u64* out_off,
                        const u32* out_len, i32* status, const u32* walk_perm, const u32* walk_hist,
                        u32 walk_classes, u32 tiny_class, u32 blocks, hipStream_t stream) {

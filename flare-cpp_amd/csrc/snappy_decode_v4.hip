@@ -105,7 +105,10 @@ static_assert(kIdxWavesSerial == 1 || kIdxWavesSerial == 2 || kIdxWavesSerial ==
 // ---- pass 1b (index_big_message, run by exec_kernel's large-message waves) geometry
 constexpr u32 kBigIndexMin = 8 * 1024;       // large: compressed size above
 constexpr u32 kBigIndexMax = 48 * 1024;      // clamp(4 x the batch mean, min, max)
-constexpr u32 kHugeIndexBytes = 256 * 1024;  // large ones handed out first
+#ifndef FSG_HUGE_KB
+#define FSG_HUGE_KB 256
+#endif
+constexpr u32 kHugeIndexBytes = FSG_HUGE_KB * 1024;  // large ones handed out first (forked: chunked walk)
 constexpr u32 kBigStageChunks = 5 * 64;      // 16-byte chunks staged per wave
 constexpr u32 kBigStageBytes = 16 * kBigStageChunks;
 
@@ -2939,7 +2942,11 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   // chunked walk alone had measured slower (the huge bodies were then off
   // the critical path).
   const bool kChunked = opt(kOptChunkedHuge) != 0;  // (the tests run both forms)
-  const u64 max_huge = chunk_bytes / 320;
+  // record region: 8 B per possible huge message (its first record, its
+  // chain verdict), then the chunk records -- sized for the batch's bound on
+  // huge messages (est_total_in / kHugeIndexBytes), the records after them
+  const u64 max_huge_need = est_total_in / kHugeIndexBytes + 1;
+  const u64 max_huge = 8 * max_huge_need < chunk_bytes ? max_huge_need : chunk_bytes / 320;
   const u64 max_recs = max_huge ? (chunk_bytes - 8 * max_huge) / sizeof(ChunkRec) : 0;
   u32* const first_rec = reinterpret_cast<u32*>(chunk_region);
   u32* const mstat = first_rec + max_huge;

@@ -156,7 +156,7 @@ def test_randomized_against_oracle(gpu, oracle, encoder):
 
 
 @pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1"), (0, "1p"), (0, "1s0"),
-                                          (0, "1s1"), (0, "1s2"), (0, "1t0")])
+                                          (0, "1s1"), (0, "1s2"), (0, "1t1")])
 def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, fsg_opts):
     """Mutated and truncated streams (64 B to 70 KB bodies).  fork "1" runs
     the path of batches over 128K messages: plan pass, the large messages'
@@ -165,10 +165,10 @@ def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, fsg_opts):
     ~150 messages (FSG_SMALL_PERSIST); "1sK" with FSG_SPLIT_WALK=K (0: the
     small bodies executed in message order; 1: walk and execution split by
     size on two streams; 2: one execution launch in walk order; default 3:
-    two execution launches by size; bodies under 512 compressed bytes one per
-    lane by the tiny-body pass, "1t0" without it)."""
+    two execution launches by size); "1t1" with the tiny-body pass (bodies
+    under 512 compressed bytes one per lane, off by default)."""
     fsg_opts(decode_fork=fork[0])
-    fsg_opts(tiny_pass=0 if fork == "1t0" else 1)
+    fsg_opts(tiny_pass=1 if fork == "1t1" else 0)
     fsg_opts(small_persist="5" if fork == "1p" else "1792")
     fsg_opts(split_walk=fork[2] if fork.startswith("1s") else "3")
     gpu.codec.select_kernels(variant, 0)
