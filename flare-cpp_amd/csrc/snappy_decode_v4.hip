@@ -65,6 +65,10 @@ constexpr int kIdxTagsOne = 32, kIdxTagsPlanned = 24;
 #ifndef FSG_BIG_TWO_WINDOWS
 #define FSG_BIG_TWO_WINDOWS 1
 #endif
+// Pass 1b's priority on the forked path's non-huge set (A/B knob; 0 = none).
+#ifndef FSG_BIG_PRIO
+#define FSG_BIG_PRIO 0
+#endif
 // The one-stream lane walk stores its bitmap four groups at a time (see
 // index_kernel).
 #ifndef FSG_IDX_SUPER
@@ -991,6 +995,10 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
   const u32 n_huge = mode == 2 ? 0u : big_count[8];
   const u32 count = (mode == 1 ? 0u : big_count[0]) + n_huge;
   if (count == 0) return;  // uniform batches: no atomics on the shared counter
+#if FSG_BIG_PRIO
+  // forked path: the longest of these walks is a side stream's critical path
+  if (mode == 2) __builtin_amdgcn_s_setprio(FSG_BIG_PRIO);
+#endif
   for (;;) {  // all-lane atomic: lane 0 adds 1, lane 0's result is the index
     const u32 got = atomicAdd(big_next, lane == 0 ? 1u : 0u);
     const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
@@ -1559,6 +1567,12 @@ namespace {
 #ifndef FSG_RB_MASK
 #define FSG_RB_MASK 0
 #endif
+#ifndef FSG_HOIST_TAG
+#define FSG_HOIST_TAG 0
+#endif
+#ifndef FSG_EARLY_A
+#define FSG_EARLY_A 1
+#endif
 #ifndef FSG_FILL_PAIRS
 #define FSG_FILL_PAIRS 0
 #endif
@@ -2079,6 +2093,7 @@ __device__ __forceinline__ void exec5_message(
   // the next group's tag bytes: 20 bytes from the dword below the tag
   u32 pf_head = 0xffffffffu, pf_cnt = 0;
   u32 pf_pos = 0;  // the ring positions the prefetch used (FSG_PF_POS)
+  u32 e_pf = 0;    // their tag-table entries (FSG_HOIST_TAG)
   u32x4 pd = u32x4{0, 0, 0, 0};
   u32 pd4 = 0;
   auto prefetch = [&](u32 p) {
@@ -2161,7 +2176,12 @@ __device__ __forceinline__ void exec5_message(
     const bool valid = lane < take0;
     // every lane reads the ring and prefetches: a lane past the valid tags
     // reads a stale position, whose buffer loads return message bytes or 0
-#if FSG_PF_POS
+#if FSG_HOIST_TAG
+    // the tag-table entry of the prefetched tags was read at the end of the
+    // last group (e_pf) unless a fill since added tags: then re-prefetch
+    const bool pf_ok = pf_head == head && pf_cnt >= take0;
+#endif
+#if FSG_PF_POS || FSG_HOIST_TAG
     // the prefetch's ring positions are this group's unless a fill added
     // tags after it: then read the ring and prefetch again
     u32 pos = pf_pos;
@@ -2180,6 +2200,8 @@ __device__ __forceinline__ void exec5_message(
     const u32 c = __builtin_amdgcn_alignbyte(pd[1], pd[0], s) & 0xffu;
 #if FSG_EXEC_TAG_VALU
     const u32 e = exec_tag_entry(c);
+#elif FSG_HOIST_TAG
+    const u32 e = pf_ok ? e_pf : tagtab[c];
 #else
     const u32 e = tagtab[c];
 #endif
@@ -2283,23 +2305,28 @@ __device__ __forceinline__ void exec5_message(
       sbase = nsb;
       zero_end = (keep + 15) & ~15u;
     }
-    // ---------- prefetch the next group's tag bytes
-    {
-      const u32 nh = head + k_tags;
-      const u32 na = tail - nh;
-      const u32 ncnt = na < 64 ? na : 64u;
-      pf_pos = ring[(nh + lane) & (kTagRing - 1)];
-      prefetch(pf_pos);
-      pf_head = nh;
-      pf_cnt = ncnt;
-    }
-    while (op + tot_len + 20 - sbase > zero_end) {
+    // ---------- prefetch the next group's tag bytes; zero the window ahead
+    auto prefetch_next_and_zero = [&]() {
+      {
+        const u32 nh = head + k_tags;
+        const u32 na = tail - nh;
+        const u32 ncnt = na < 64 ? na : 64u;
+        pf_pos = ring[(nh + lane) & (kTagRing - 1)];
+        prefetch(pf_pos);
+        pf_head = nh;
+        pf_cnt = ncnt;
+      }
+      while (op + tot_len + 20 - sbase > zero_end) {
 #ifndef FSG_KO_ZERO
-      zero_from(zero_end);
+        zero_from(zero_end);
 #endif
-      zero_end += 1024;
-    }
-    wave_lds_fence();
+        zero_end += 1024;
+      }
+      wave_lds_fence();
+    };
+#if !FSG_EARLY_A
+    prefetch_next_and_zero();
+#endif
 
     STAMP(2);
     // ---------- chunks: a literal's all come in round A (registers for
@@ -2359,6 +2386,13 @@ __device__ __forceinline__ void exec5_message(
     const u64 m1 = __ballot(kf > 1);
 #ifndef FSG_KO_LOADS
     if (m1 && kf > 1) gload(1, a1, a1e);
+#endif
+#if FSG_EARLY_A
+    // (the round-A loads go out before the next group's ring read and tag
+    // prefetch and the window zeroing: their latency is the group's longest
+    // wait; the near-ready LDS reads above read bytes below op, which the
+    // zeroing (from zero_end >= op) does not touch)
+    prefetch_next_and_zero();
 #endif
     if (prio) __builtin_amdgcn_s_setprio(0);
     STAMP(3);
@@ -2476,6 +2510,11 @@ __device__ __forceinline__ void exec5_message(
     }
     op += tot_len;
     head += k_tags;
+#if FSG_HOIST_TAG
+    // the next group's tag-table entries, now: the prefetched tag bytes have
+    // long landed, and the read's latency overlaps the loop's head
+    e_pf = tagtab[__builtin_amdgcn_alignbyte(pd[1], pd[0], (pf_pos + ibal) & 3u) & 0xffu];
+#endif
     STAMP(6);
   }
   if (op != op1) {  // the stream ended early (snappy.cc:858-868)
