@@ -49,6 +49,25 @@ namespace {
 
 constexpr u32 kPredNone = 0xff, kPredUnknown = 0xfe;
 
+// The event loop's fast path (see wave_fragment); 0 = the general path only
+// (A/B builds).
+#ifndef FSG_WENC_FAST
+#define FSG_WENC_FAST 1
+#endif
+// Output bytes stored straight to global memory (no LDS staging ring) and
+// the in-block predecessors found without a scratch array (see the pred
+// rounds), so the table is the wave's only LDS: five 32 KiB tables per CU
+// instead of four.  0 = the staging ring and the pred scratch (A/B builds).
+#ifndef FSG_WENC_DIRECT
+#define FSG_WENC_DIRECT 1
+#endif
+// (ds_write_b8 into the staging ring, or a byte store to the output)
+#if FSG_WENC_DIRECT
+#define OUTB(i) obase[(i)]
+#else
+#define OUTB(i) stg[(i) & 511]
+#endif
+
 // Diagnostic build only (-DFSG_STAMPS): per-phase cycle totals of the wave
 // encoder, summed over waves (fsg_debug_wstamps).
 #ifdef FSG_STAMPS
@@ -153,6 +172,10 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
   u32 opos = 0, flushed = 0;
   auto room = [&](u32 bytes) -> bool { return cap == 0xffffffffu || opos + bytes + 16 <= cap; };
   auto flush_to = [&](u32 upto) {
+#if FSG_WENC_DIRECT
+    flushed = upto;
+    return;
+#endif
     lds_fence();
     for (u32 b0 = flushed; b0 < upto; b0 += 64) {
       const u32 i = b0 + lane;
@@ -162,7 +185,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
   };
   // nb (1..5) tag bytes, one lane per byte
   auto put_tag = [&](u64 tag, u32 nb) {
-    if (lane < nb) stg[(opos + lane) & 511] = (u8)(tag >> (8 * (lane & 7)));
+    if (lane < nb) OUTB(opos + lane) = (u8)(tag >> (8 * (lane & 7)));
     opos += nb;
   };
   // literal [s, e): tag, then the bytes from the lanes holding them (this
@@ -178,10 +201,10 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
     }
     if (s >= B || (prev_ok && s + 64 >= B)) {
       const u32 qc = B + lane;
-      if (qc >= s && qc < e) stg[(opos + qc - s) & 511] = (u8)xw0c;
+      if (qc >= s && qc < e) OUTB(opos + qc - s) = (u8)xw0c;
       if (prev_ok) {
         const u32 qp = B - 64 + lane;
-        if (qp >= s && qp < e) stg[(opos + qp - s) & 511] = (u8)xw0p;
+        if (qp >= s && qp < e) OUTB(opos + qp - s) = (u8)xw0p;
       }
       opos += len;
     } else {
@@ -270,7 +293,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       if (r < tle) byte = ltv >> (8 * r);
       else if (r < tle + le) byte = x < 64 ? bp : bc;
       else byte = ctv >> (8 * ((r - tle - le) & 3));
-      if (j < total) stg[(opos + j) & 511] = (u8)byte;
+      if (j < total) OUTB(opos + j) = (u8)byte;
     }
     opos += total;
     nev = 0;
@@ -361,6 +384,34 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       }
       STAMP(1);
       // ---- pred rounds (the table slots are restored by the commit)
+#if FSG_WENC_DIRECT
+      // Every active lane writes its position into its slot (highest lane
+      // wins) and reads it back; the winners leave and listen one more
+      // round: what they read then is the winner of that round among their
+      // hash's remaining lanes -- the nearest lane below them with their
+      // hash, their predecessor -- or their own position if none remain.
+      // After a fourth round the lanes still in it are unknown (a chain of
+      // five or more; resolved by a scan when probed).
+      u32 p1 = kPredNone;
+      {
+        bool active = true, listen = false;
+        for (int r = 0; r < 4; ++r) {
+          if (!__ballot(active)) break;
+          if (active) table[h] = (u16)(B + lane);
+          lds_fence();
+          const u32 rb = (active || listen) ? (u32)table[h] : 0u;
+          lds_fence();
+          if (listen) p1 = rb != B + lane ? rb - B : (u32)kPredNone;
+          if (r == 3) {
+            if (active) p1 = kPredUnknown;
+            break;
+          }
+          const bool win = active && rb == B + lane;
+          listen = win;
+          active = active && !win;
+        }
+      }
+#else
       pscr[lane] = (u8)kPredNone;
       lds_fence();
       {
@@ -386,9 +437,10 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
           lds_fence();
         }
       }
+      const u32 p1 = pscr[lane];
+#endif
       // (ds_bpermute reads 0 from a lane outside EXEC, so every permute runs
       // on all lanes and the selects come after)
-      const u32 p1 = pscr[lane];
       const u32 t2 = bperm(p1, p1 & 63);
       const u32 p2 = p1 < 64 ? t2 : p1;
       const u32 X1 = bperm(X, p1 & 63);
@@ -437,6 +489,59 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
 
       bool done = false, leave = false;
       for (u32 ev = 0; !done && !leave && ev < 200; ++ev) {
+#if FSG_WENC_FAST
+        // ---- fast events: the common case of text, taken without the
+        // general path's machinery (ISA: ~25 scalar instructions and two
+        // readlanes per event instead of ~70 and a branch tree).  From the
+        // post-copy state: the probe at ip (snappy.cc:428-438) by a lane with
+        // no in-block predecessor; if it misses, the stride-1 probes of the
+        // literal search (skip 32..63, snappy.cc:377-397) up to their first
+        // T-match, with no predecessor lane among the probes before it; a
+        // match shorter than the 20 compared bytes; literal bytes in
+        // registers.  Any other case leaves the state untouched and falls
+        // through to the general event below, which decides it exactly.
+        while (post && ev < 200) {
+          const u32 k0 = ip - B;  // < 64: the block holds ip (else leave)
+          if (!((Stat >> k0) & 1ull)) break;
+          u32 fpk = rl(packT, k0);
+          u64 nI = I | (1ull << k0);
+          u32 fq = ip;
+          if (!(fpk >> 31)) {
+            const u32 a = k0 + 1;  // the search starts at ip + 1 with skip 32
+            if (a >= 64) break;
+            const u32 c = 64 - a < 32 ? 64 - a : 32u;
+            const u32 fp = ip + 1;
+            if ((lim >= fp ? lim - fp : 0u) < c) break;
+            const u64 S = ((1ull << c) - 1) << a;
+            const u64 Mst = S & Stat & MTb;
+            if (!Mst) break;
+            const u32 ks = (u32)__builtin_ctzll(Mst);
+            const u64 below = (1ull << ks) - 1;
+            if (S & ~Stat & below) break;
+            fpk = rl(packT, ks);
+            fq = B + ks;
+            nI |= S & ((below << 1) | 1ull);
+          }
+          u32 fml = (fpk >> 16) & 31u;
+          if (fml >= 20 && fq + 20 < n) break;
+          if (fml > n - fq) fml = n - fq;
+          const u32 L = fq - next_emit;
+          if (!(L == 0 || next_emit >= B || (prev_ok && next_emit + 64 >= B))) break;
+          const bool mine = lane == nev;
+          EQL = mine ? fq | (L << 16) : EQL;
+          ECM = mine ? (fpk & 0xffffu) | (fml << 16) : ECM;
+          ++nev;
+          ++ev;
+          I = nI;
+          ip = fq + fml;
+          next_emit = ip;
+          WCOUNT(9);
+          if (ip >= lim) { done = true; break; }
+          if (ip - 1 < B + 64) I |= 1ull << (ip - 1 - B);
+          if (ip >= B + 64) { leave = true; break; }
+        }
+        if (done || leave || ev >= 200) break;
+#endif
         u32 q = 0, pk = 0;
         bool found = false;
         if (post) {
@@ -623,8 +728,13 @@ __global__ __launch_bounds__(64) void encode_wave_kernel(
     u32* __restrict__ ctr, const u32* __restrict__ items, u32* __restrict__ sizes, u32 region_cap,
     u32 share_permille, u64 all_bytes) {
   extern __shared__ __attribute__((aligned(16))) u16 wtab[];
+#if FSG_WENC_DIRECT
+  u8* const pscr = nullptr;
+  u8* const stg = nullptr;
+#else
   __shared__ u8 pscr[64];
   __shared__ __attribute__((aligned(16))) u8 stg[512];
+#endif
   const u32 lane = threadIdx.x;
   const u32 quota = (u32)__builtin_amdgcn_readfirstlane((int)wave_quota(ctr, share_permille, all_bytes));
   (void)n_msgs;
@@ -682,5 +792,8 @@ __global__ __launch_bounds__(64) void encode_wave_kernel(
 // LDS bytes of encode_wave_kernel's table for a batch whose largest fragment
 // is max_frag bytes.
 size_t encode_wave_lds_bytes(u32 max_frag) { return (size_t)table_size_for(max_frag) * sizeof(u16); }
+// Static LDS of encode_wave_kernel besides the table (the staging ring and
+// the pred scratch when FSG_WENC_DIRECT is off), for the launch's waves per CU.
+size_t encode_wave_static_lds_bytes() { return FSG_WENC_DIRECT ? 0 : 640; }
 
 }  // namespace fsg

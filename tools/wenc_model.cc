@@ -30,7 +30,7 @@ static inline u32 hashb(u32 x, int shift) { return (x * kHashMul) >> shift; }
 
 struct Stats {
   u64 blocks = 0, events = 0, probes = 0, pred_rounds = 0, deep = 0, slow_resolve = 0, long_match = 0,
-      jumps = 0, direct_inserts = 0, frags = 0;
+      jumps = 0, direct_inserts = 0, frags = 0, fast = 0;
 } st;
 static int g_trace = 0;
 
@@ -196,8 +196,12 @@ static u8* wenc_fragment(const u8* f, u32 n, u8* op, u16* table, u32 ht) {
       while (!done && !leave) {
         u32 q = 0, cand = 0;
         bool found = false;
+        // would the kernel's fast event path (FSG_WENC_FAST) take this event?
+        bool fast_ok = mode == POST;
+        const u32 ip_at = ip;
         if (mode == POST) {
           const int k0 = (int)(ip - B);
+          fast_ok = fast_ok && pred1[k0] == -1;
           cand = resolve(k0, I);
           I |= 1ull << k0;
           st.probes++;
@@ -218,6 +222,7 @@ static u8* wenc_fragment(const u8* f, u32 n, u8* op, u16* table, u32 ht) {
             const u32 step = sk >> 5;
             if (p + step > lim) { done = true; break; }
             const int k = (int)(p - B);
+            fast_ok = fast_ok && pred1[k] == -1 && p - ip_at <= 32 && sk < 64;
             cand = resolve(k, I);
             I |= 1ull << k;
             st.probes++;
@@ -241,6 +246,7 @@ static u8* wenc_fragment(const u8* f, u32 n, u8* op, u16* table, u32 ht) {
         u32 m = 4;
         while (q + m < n && f[cand + m] == f[q + m]) ++m;
         if (m > 20) st.long_match++;
+        if (fast_ok && (m < 20 || q + 20 >= n)) st.fast++;
         if (g_trace) printf("copy %u %u %u\n", q, cand, m);
         op = emit_copy(op, q - cand, m);
         ip = q + m;
@@ -368,6 +374,20 @@ int main(int argc, char** argv) {
     std::vector<u8> x(65536), o(so_max_compressed_length(65536) + 64);
     dg_text_body(t * 257, x.data(), x.size());
     wenc_compress(x.data(), x.size(), o.data());
+  }
+  printf("C3 fast-path events %.1f%%\n", 100.0 * st.fast / st.events);
+  {
+    Stats c3 = st;
+    st = Stats();
+    for (u32 t = 0; t < 300; ++t) {
+      std::vector<u8> x(70000 + 64), o(so_max_compressed_length(70064) + 64);
+      const size_t nn = dg_snappy_message(t * 31, 16384 + (u32)(rnd() % 48000), x.data());
+      wenc_compress(x.data(), nn, o.data());
+    }
+    printf("proto 16-64K: events %.2f/block probes %.2f/block pred_rounds %.2f/block slow %llu fast-path events %.1f%%\n",
+           (double)st.events / st.blocks, (double)st.probes / st.blocks, (double)st.pred_rounds / st.blocks,
+           (unsigned long long)st.slow_resolve, 100.0 * st.fast / st.events);
+    st = c3;
   }
   printf("C3: blocks %.1f/frag events %.2f/block probes %.2f/block pred_rounds %.2f/block slow %llu kernel-slow %llu long %llu "
          "jumps %llu\n",
