@@ -49,10 +49,12 @@ namespace {
 
 constexpr u32 kPredNone = 0xff, kPredUnknown = 0xfe;
 
-// The event loop's fast path (see wave_fragment); 0 = the general path only
-// (A/B builds).
+// The event loop's fast path (see wave_fragment): 2 = each lane precomputes
+// the event of a post-copy arrival at its position, and the walk follows
+// them; 1 = the same rules evaluated event by event; 0 = the general path
+// only (A/B builds).
 #ifndef FSG_WENC_FAST
-#define FSG_WENC_FAST 1
+#define FSG_WENC_FAST 2
 #endif
 // Output bytes stored straight to global memory (no LDS staging ring) and
 // the in-block predecessors found without a scratch array (see the pred
@@ -259,15 +261,40 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
 
   // ---- deferred emission: the block's common events (a literal whose bytes
   // are in this block's or the previous block's registers, a copy of <= 64
-  // bytes) are recorded one per lane (lane nev: q | literal length << 16,
-  // candidate | match length << 16) and written together: sizes, a prefix
-  // sum, then one output byte per lane.  Other events flush the recorded ones
-  // first and take the paths above.
-  u32 EQL = 0, ECM = 0, nev = 0;
-  auto emit_pending = [&](u32 B, u32 xw0c, u32 xw0p) -> bool {
-    if (!nev) return true;
-    const u32 q = EQL & 0xffffu, L = EQL >> 16, cand = ECM & 0xffffu, ml = ECM >> 16;
-    const bool ve = lane < nev;
+  // bytes) are recorded one per lane -- in the lane of the event's first
+  // parse position (the post-copy probe, or the search start), so events sit
+  // in increasing lanes, EvM marking them: q | literal length << 16,
+  // candidate | match length << 16 (fast events: the lane's precomputed
+  // fEQL / fECM, FastEv) -- and written together: sizes, a prefix sum over
+  // the lanes, then one output byte per lane.  Other events flush the
+  // recorded ones first and take the paths above.
+  u32 EQL = 0, ECM = 0, fEQL = 0, fECM = 0;
+  u64 EvM = 0, FastEv = 0;
+#if FSG_WENC_DIRECT
+  // A block's commit-time output (<= 128 bytes: one byte per lane in two
+  // registers) is held until the next block has waited for its input and
+  // issued its loads, then stored by two unconditional buffer stores (lanes
+  // past the count store out of range, which the buffer drops).  Stored at
+  // once, it would sit in the wave's one memory counter ahead of the next
+  // block's input loads, and the wait for those loads would wait for the
+  // stores too.
+  u32 held0 = 0, held1 = 0, held_n = 0, held_at = 0;
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      obase, (short)0, (int)(cap != 0xffffffffu ? cap : (u32)max_compressed_length(n)), 0x00020000);
+  auto store_held = [&]() {
+    const u32 o0 = lane < held_n ? held_at + lane : 0x80000000u;
+    const u32 o1 = lane + 64 < held_n ? held_at + 64 + lane : 0x80000000u;
+    __builtin_amdgcn_raw_buffer_store_b8((u8)held0, orsrc, (int)o0, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((u8)held1, orsrc, (int)o1, 0, 0);
+    held_n = 0;
+  };
+#endif
+  auto emit_pending = [&](u32 B, u32 xw0c, u32 xw0p, bool hold = false) -> bool {
+    if (!EvM) return true;
+    const bool fe = (FastEv >> lane) & 1ull;
+    const u32 eql = fe ? fEQL : EQL, ecm = fe ? fECM : ECM;
+    const u32 q = eql & 0xffffu, L = eql >> 16, cand = ecm & 0xffffu, ml = ecm >> 16;
+    const bool ve = (EvM >> lane) & 1ull;
     const u32 nm1 = L - 1;
     const u32 tl = L == 0 ? 0u : (nm1 < 60 ? 1u : 2u);  // L <= 128 here
     const u32 lt = nm1 < 60 ? nm1 << 2 : (240u | (nm1 << 8));
@@ -283,8 +310,11 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
     const u32 A = excl | (tl << 12) | (L << 14) | ((q - L - (B - 64)) << 22);
     for (u32 j0 = 0; j0 < total; j0 += 64) {
       const u32 j = j0 + lane;
-      u32 e = 0;
-      for (u32 k = 1; k < nev; ++k) e = j >= rl(excl, k) ? k : e;
+      u32 e = (u32)__builtin_ctzll(EvM);
+      for (u64 mm = EvM & (EvM - 1); mm; mm &= mm - 1) {
+        const u32 k = (u32)__builtin_ctzll(mm);
+        e = j >= rl(excl, k) ? k : e;
+      }
       const u32 a = bperm(A, e), ltv = bperm(lt, e), ctv = bperm(ct, e);
       const u32 r = j - (a & 0xfffu), tle = (a >> 12) & 3u, le = (a >> 14) & 0xffu, xs = a >> 22;
       const u32 x = xs + (r - tle);  // literal byte's position relative to B - 64
@@ -293,10 +323,24 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       if (r < tle) byte = ltv >> (8 * r);
       else if (r < tle + le) byte = x < 64 ? bp : bc;
       else byte = ctv >> (8 * ((r - tle - le) & 3));
+#if FSG_WENC_DIRECT
+      if (hold && total <= 128) {
+        if (j0 == 0) held0 = byte;
+        else held1 = byte;
+        continue;
+      }
+#endif
       if (j < total) OUTB(opos + j) = (u8)byte;
     }
+#if FSG_WENC_DIRECT
+    if (hold && total <= 128) {
+      held_n = total;
+      held_at = opos;
+    }
+#endif
     opos += total;
-    nev = 0;
+    EvM = 0;
+    FastEv = 0;
     return true;
   };
 
@@ -354,7 +398,18 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       // ---- table slots and candidate bytes
       const u32 X = xw.w[0];
       const u32 h = (X * kHashMul) >> shift;
+      const u32 h1 = (xw1.w[0] * kHashMul) >> shift;
+      // (the LDS reads of this block's slots, the next block's speculative
+      // slots and the first pred round go out together: one wait)
       const u32 T = table[h];
+      const u32 Tn_next = table[h1];
+#if FSG_WENC_DIRECT
+      lds_fence();
+      table[h] = (u16)(B + lane);
+      lds_fence();
+      const u32 rb0 = table[h];
+      lds_fence();
+#endif
       W5 cb;
       {
         // the speculative loads are right unless the previous block changed the slot
@@ -365,23 +420,29 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
 #pragma unroll
         for (int i = 0; i < 5; ++i) pb.w[i] = bperm(xwp.w[i], src);
         const bool need_load = fix && !inprev;
-        Raw20 rr{};
-        if (__ballot(need_load)) rr = raw20(fr, fal + (need_load ? T : 0u));
         const W5 sp = spec ? shifted20(cbn) : W5{};
-        const W5 ld = shifted20(rr);
 #pragma unroll
-        for (int i = 0; i < 5; ++i) cb.w[i] = !fix ? sp.w[i] : (inprev ? pb.w[i] : ld.w[i]);
+        for (int i = 0; i < 5; ++i) cb.w[i] = !fix ? sp.w[i] : pb.w[i];
+        // (the load and its wait stay inside the branch: a wait after the
+        // join would be counted for the branch-taken path and, on the
+        // common path, wait for the input loads issued just before)
+        if (__ballot(need_load)) {
+          const Raw20 rr = raw20(fr, fal + (need_load ? T : 0u));
+          const W5 ld = shifted20(rr);
+#pragma unroll
+          for (int i = 0; i < 5; ++i) cb.w[i] = need_load ? ld.w[i] : cb.w[i];
+        }
       }
       // ---- the next block's slots and candidate loads, speculative: read
       // before this block's pred rounds and commit, so a slot that differs at
       // the next block's start was written by this block's commit (a position
       // of this block: its bytes come from these lanes by ds_bpermute)
-      {
-        const u32 h1 = (xw1.w[0] * kHashMul) >> shift;
-        Tn = table[h1];
-        cbn = raw20(fr, fal + Tn);
-        spec = true;
-      }
+      Tn = Tn_next;
+      cbn = raw20(fr, fal + Tn);
+      spec = true;
+#if FSG_WENC_DIRECT
+      store_held();  // the previous block's output (see held0)
+#endif
       STAMP(1);
       // ---- pred rounds (the table slots are restored by the commit)
 #if FSG_WENC_DIRECT
@@ -391,16 +452,20 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       // hash's remaining lanes -- the nearest lane below them with their
       // hash, their predecessor -- or their own position if none remain.
       // After a fourth round the lanes still in it are unknown (a chain of
-      // five or more; resolved by a scan when probed).
+      // five or more; resolved by a scan when probed).  Round 1 went out
+      // with the slot reads above.
       u32 p1 = kPredNone;
       {
         bool active = true, listen = false;
+        u32 rb = rb0;
         for (int r = 0; r < 4; ++r) {
-          if (!__ballot(active)) break;
-          if (active) table[h] = (u16)(B + lane);
-          lds_fence();
-          const u32 rb = (active || listen) ? (u32)table[h] : 0u;
-          lds_fence();
+          if (r > 0) {
+            if (!__ballot(active)) break;
+            if (active) table[h] = (u16)(B + lane);
+            lds_fence();
+            rb = (active || listen) ? (u32)table[h] : 0u;
+            lds_fence();
+          }
           if (listen) p1 = rb != B + lane ? rb - B : (u32)kPredNone;
           if (r == 3) {
             if (active) p1 = kPredUnknown;
@@ -487,9 +552,66 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
         return scan(j, Ims);
       };
 
+#if FSG_WENC_FAST == 2
+      // ---- fast events, precomputed per lane k: the event a post-copy
+      // arrival at B + k makes under the fast rules (snappy.cc:428-438 and
+      // the stride-1 probes of :377-397): the probe at B + k by a lane with
+      // no in-block predecessor; if it misses, the probes B+k+1 .. B+k+c
+      // (skip 32..63) up to their first T-match, no predecessor lane among
+      // those before it; a match shorter than the 20 compared bytes.  Kept:
+      // the next parse position, the inserted lanes, the event record, and
+      // FastM, the lanes whose arrival the rules decide.
+      u32 fsucc, filo, fihi;
+      u64 FastM;
+      {
+        const u64 SM = Stat & MTb, NS = ~Stat;
+        const u32 k = lane;
+        const u32 c = 63 - k < 32 ? 63 - k : 32u;
+        const u64 S = k < 63 ? ((1ull << c) - 1) << (k + 1) : 0ull;
+        const u64 Mst = S & SM;
+        const u32 ks = (u32)__builtin_ctzll(Mst | 0x8000000000000000ull);
+        const u64 below = (1ull << ks) - 1;
+        const bool hit = packT >> 31;
+        const bool miss_ok = Mst != 0 && (S & NS & below) == 0 && (int)lim - (int)(B + k) - 1 >= (int)c;
+        const u32 pks = bperm(packT, ks);
+        const u32 fpk = hit ? packT : pks;
+        const u32 fq = hit ? B + k : B + ks;
+        u32 fml = (fpk >> 16) & 31u;
+        const bool lng = fml >= 20 && fq + 20 < n;
+        fml = fml < n - fq ? fml : n - fq;
+        const u64 Iadd = (1ull << k) | (hit ? 0ull : S & ((below << 1) | 1ull));
+        fsucc = fq + fml;
+        filo = (u32)Iadd;
+        fihi = (u32)(Iadd >> 32);
+        fEQL = fq | ((fq - (B + k)) << 16);
+        fECM = (fpk & 0xffffu) | (fml << 16);
+        FastM = __ballot(((Stat >> k) & 1ull) && (hit || miss_ok) && !lng);
+      }
+#endif
       bool done = false, leave = false;
       for (u32 ev = 0; !done && !leave && ev < 200; ++ev) {
-#if FSG_WENC_FAST
+#if FSG_WENC_FAST == 2
+        // ---- fast events (see the per-lane precomputation above): a walk
+        // over the lanes' successors while the arrival lane's event is fast
+        while (post && ev < 200) {
+          const u32 k0 = ip - B;  // < 64: the block holds ip (else leave)
+          if (!((FastM >> k0) & 1ull)) break;
+          const u32 nip = rl(fsucc, k0);
+          I |= ((u64)rl(fihi, k0) << 32) | (u64)rl(filo, k0);
+          const u64 kb = 1ull << k0;
+          EvM |= kb;
+          FastEv |= kb;
+          ++ev;
+          ip = nip;
+          next_emit = ip;
+          WCOUNT(9);
+          if (ip >= lim) { done = true; break; }
+          const u32 im1 = ip - 1 - B;
+          if (im1 < 64) I |= 1ull << im1;
+          if (ip >= B + 64) { leave = true; break; }
+        }
+        if (done || leave || ev >= 200) break;
+#elif FSG_WENC_FAST
         // ---- fast events: the common case of text, taken without the
         // general path's machinery (ISA: ~25 scalar instructions and two
         // readlanes per event instead of ~70 and a branch tree).  From the
@@ -527,10 +649,10 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
           if (fml > n - fq) fml = n - fq;
           const u32 L = fq - next_emit;
           if (!(L == 0 || next_emit >= B || (prev_ok && next_emit + 64 >= B))) break;
-          const bool mine = lane == nev;
+          const bool mine = lane == k0;
           EQL = mine ? fq | (L << 16) : EQL;
           ECM = mine ? (fpk & 0xffffu) | (fml << 16) : ECM;
-          ++nev;
+          EvM |= 1ull << k0;
           ++ev;
           I = nI;
           ip = fq + fml;
@@ -544,6 +666,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
 #endif
         u32 q = 0, pk = 0;
         bool found = false;
+        const u32 key = (post ? ip : p) - B;  // the event's lane (see EvM)
         if (post) {
           // the probe right after a copy (snappy.cc:428-438), lane k0
           const u32 k0 = ip - B;
@@ -651,10 +774,10 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
           const u32 L = q - next_emit;
           const bool lit_regs = L == 0 || next_emit >= B || (prev_ok && next_emit + 64 >= B);
           if (lit_regs && mlen <= 64) {
-            const bool mine = lane == nev;
+            const bool mine = lane == key;
             EQL = mine ? q | (L << 16) : EQL;
             ECM = mine ? cand | (mlen << 16) : ECM;
-            ++nev;
+            EvM |= 1ull << key;
           } else {
             if (!emit_pending(B, X, xwp.w[0])) return nullptr;
             if (L) {
@@ -681,7 +804,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       lds_fence();
       if ((I >> lane) & 1ull) table[h] = (u16)(B + lane);
       lds_fence();
-      if (!emit_pending(B, X, xwp.w[0])) return nullptr;
+      if (!emit_pending(B, X, xwp.w[0], true)) return nullptr;
       pend_end = opos;
       STAMP(5);
       WCOUNT(8);
@@ -691,6 +814,9 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       if ((npos & ~63u) != B + 64) spec = false;
     }
   }
+#if FSG_WENC_DIRECT
+  store_held();  // the last block's output
+#endif
   if (next_emit < n) {
     if (!room(n - next_emit + 5)) return nullptr;
     // remainder (snappy.cc:446-450): bytes from global memory
