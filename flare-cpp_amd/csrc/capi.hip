@@ -83,7 +83,7 @@ constexpr OptDesc kOptDesc[fsg::kOptCount] = {
     {"diag_no_tail", "FSG_DIAG_NO_TAIL", 0},
     {"tiny_pass", "FSG_TINY_PASS", 0},
     {"encode_wave_min", "FSG_ENCODE_WAVE_MIN", 16384},
-    {"encode_wave_share", "FSG_ENCODE_WAVE_SHARE", 280},
+    {"encode_wave_share", "FSG_ENCODE_WAVE_SHARE", 500},
     {"encode_wave_all_mb", "FSG_ENCODE_WAVE_ALL_MB", 640},
     {"encode_lanes", "FSG_ENCODE_LANES", 0},
     {"lz4_big_min", "FSG_L4_BIG_MIN", -1},

@@ -91,10 +91,11 @@ constexpr u32 kWholeUnit = 0x80000000u;  // unit = a whole message (not a fragme
 // lane encoder.  All of them when their bytes fit what the wave encoder does
 // in about the time one lane needs for a 64 KiB fragment at full load (the
 // lane path's floor: a lane taking a long unit late sets the batch's tail;
-// measured on MI355X: wave encoder ~15.9 GB/s on text, one lane ~40 ms per
-// 64 KiB fragment); otherwise the wave encoder's share of a bandwidth-bound
-// batch (~0.28: 15.9 GB/s beside the lanes' ~40 GB/s).  Both kernels compute
-// it from the plan pass's counters.
+// measured on MI355X: one lane ~40 ms per 64 KiB fragment); otherwise the
+// wave encoder's share of a bandwidth-bound batch (0.5 since round 5: the
+// wave encoder alone does C3 in ~165 ms, the lanes in ~135 ms, and a sweep
+// of 280 / 400 / 500 / 600 permille measured 97-101 / 94 / 87 / 101 ms).
+// Both kernels compute it from the plan pass's counters.
 __device__ __forceinline__ u32 wave_quota(const u32* ctr, u32 share_permille, u64 all_bytes) {
   const u32 n_long = ctr[1];
   const u64 bytes = *reinterpret_cast<const unsigned long long*>(ctr + 6);

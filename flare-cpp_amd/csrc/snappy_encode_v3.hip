@@ -668,7 +668,7 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
   // (options encode_wave_share / encode_wave_all_mb: the tests force the lane
   // share with encode_wave_all_mb 0)
   const i64 share_opt = opt(kOptEncodeWaveShare), all_opt = opt(kOptEncodeWaveAllMb);
-  const u32 kShare = share_opt >= 0 && share_opt <= 1000 ? (u32)share_opt : 280u;  // permille
+  const u32 kShare = share_opt >= 0 && share_opt <= 1000 ? (u32)share_opt : 500u;  // permille
   const u64 kAllBytes = (all_opt >= 0 && all_opt < (1 << 24) ? (u64)all_opt : 640ull) << 20;
   auto pipe = max_in_len > kBlockSize || max_in_len == 0
                   ? encode_pipe_kernel<FSG_V3_PROBES_SPLIT, FSG_V3_POST_PROBES_SPLIT>

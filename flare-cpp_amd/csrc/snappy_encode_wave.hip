@@ -73,7 +73,7 @@ constexpr u32 kPredNone = 0xff, kPredUnknown = 0xfe;
 // Diagnostic build only (-DFSG_STAMPS): per-phase cycle totals of the wave
 // encoder, summed over waves (fsg_debug_wstamps).
 #ifdef FSG_STAMPS
-__device__ unsigned long long g_wstamps[12];  // 0-7 cycles per phase, 8-11 counts
+__device__ unsigned long long g_wstamps[16];  // 0-7 cycles per phase, 8-11 counts, 12-13 cycles
 #define STAMP(k) do { const u64 t_ = __builtin_amdgcn_s_memtime(); st_[k] += t_ - t_last_; t_last_ = t_; } while (0)
 #define WCOUNT(k) (st_[k] += 1)
 #else
@@ -164,7 +164,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
                              u16* table, u32 ht, u8* pscr, u8* stg, u32 lane) {
   const int shift = 32 - (31 - __builtin_clz(ht));
 #ifdef FSG_STAMPS
-  u64 st_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  u64 st_[16] = {};
   u64 t_last_ = __builtin_amdgcn_s_memtime();
 #endif
   // zeroed table (snappy.cc:247-271)
@@ -579,7 +579,10 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
         u32 fml = (fpk >> 16) & 31u;
         const bool lng = fml >= 20 && fq + 20 < n;
         fml = fml < n - fq ? fml : n - fq;
-        const u64 Iadd = (1ull << k) | (hit ? 0ull : S & ((below << 1) | 1ull));
+        // (plus the insert of the next arrival's ip - 1, snappy.cc:432-434,
+        // when it lies in the block; after the input limit it is never read)
+        const u32 im1 = fq + fml - 1 - B;
+        const u64 Iadd = (1ull << k) | (hit ? 0ull : S & ((below << 1) | 1ull)) | (im1 < 64 ? 1ull << im1 : 0ull);
         fsucc = fq + fml;
         filo = (u32)Iadd;
         fihi = (u32)(Iadd >> 32);
@@ -587,28 +590,35 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
         fECM = (fpk & 0xffffu) | (fml << 16);
         FastM = __ballot(((Stat >> k) & 1ull) && (hit || miss_ok) && !lng);
       }
+      STAMP(12);
 #endif
       bool done = false, leave = false;
       for (u32 ev = 0; !done && !leave && ev < 200; ++ev) {
 #if FSG_WENC_FAST == 2
         // ---- fast events (see the per-lane precomputation above): a walk
-        // over the lanes' successors while the arrival lane's event is fast
-        while (post && ev < 200) {
-          const u32 k0 = ip - B;  // < 64: the block holds ip (else leave)
-          if (!((FastM >> k0) & 1ull)) break;
-          const u32 nip = rl(fsucc, k0);
-          I |= ((u64)rl(fihi, k0) << 32) | (u64)rl(filo, k0);
-          const u64 kb = 1ull << k0;
-          EvM |= kb;
-          FastEv |= kb;
-          ++ev;
+        // over the lanes' successors while the arrival lane's event is fast,
+        // up to the first arrival past the block or the input limit
+        if (post && ((FastM >> (ip - B)) & 1ull)) {
+          const u32 stop = lim < B + 64 ? lim : B + 64;
+          u32 k0 = ip - B, nip;
+          u64 evs = 0, iadd = 0;
+          for (;;) {
+            nip = rl(fsucc, k0);
+            iadd |= ((u64)rl(fihi, k0) << 32) | (u64)rl(filo, k0);
+            evs |= 1ull << k0;
+            if (nip >= stop) break;
+            k0 = nip - B;
+            if (!((FastM >> k0) & 1ull)) break;
+          }
+          I |= iadd;
+          EvM |= evs;
+          FastEv |= evs;
+          ev += (u32)__builtin_popcountll(evs);
           ip = nip;
           next_emit = ip;
-          WCOUNT(9);
-          if (ip >= lim) { done = true; break; }
-          const u32 im1 = ip - 1 - B;
-          if (im1 < 64) I |= 1ull << im1;
-          if (ip >= B + 64) { leave = true; break; }
+          done = ip >= lim;
+          leave = !done && ip >= B + 64;
+          STAMP(13);
         }
         if (done || leave || ev >= 200) break;
 #elif FSG_WENC_FAST
@@ -826,7 +836,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
   STAMP(6);
 #ifdef FSG_STAMPS
   if (lane == 0)
-    for (int k = 0; k < 12; ++k) atomicAdd(&g_wstamps[k], (unsigned long long)st_[k]);
+    for (int k = 0; k < 16; ++k) atomicAdd(&g_wstamps[k], (unsigned long long)st_[k]);
 #endif
   return obase + opos;
 }
@@ -835,7 +845,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
 extern "C" int fsg_debug_wstamps(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), sizeof(g_wstamps));
   if (reset) {
-    unsigned long long z[12] = {};
+    unsigned long long z[16] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wstamps), z, sizeof(z));
   }
   return e == hipSuccess ? 0 : -1;

@@ -43,7 +43,7 @@ def main():
     d_co, d_cl = H(coff), torch.zeros(n, dtype=torch.int32, device=dev)
     d_st = torch.zeros(n, dtype=torch.int32, device=dev)
     ws = codec.compress_workspace(n, size)
-    buf = (ctypes.c_ulonglong * 12)()
+    buf = (ctypes.c_ulonglong * 16)()
     for _ in range(2):
         if STAMPS:
             lib.fsg_debug_wstamps(buf, 1)
@@ -56,13 +56,13 @@ def main():
         print(f"messages={n} size={size} time={ev0.elapsed_time(ev1):.2f} ms")
         return
     lib.fsg_debug_wstamps(buf, 1)
-    tot = sum(buf[k] for k in range(8))
+    tot = sum(buf[k] for k in range(8)) + buf[12] + buf[13]
     blocks = max(1, buf[8])
     print(f"messages={n} size={size} time={ev0.elapsed_time(ev1):.2f} ms total wave-cycles={tot:.3e} "
           f"per fragment={tot / n:.0f} per block={tot / blocks:.0f}")
     print(f"  blocks={buf[8]} events/block={buf[9] / blocks:.2f} scans/block={buf[10] / blocks:.3f} "
           f"scan steps/block={buf[11] / blocks:.2f}")
-    for k, name in enumerate(PHASES):
+    for k, name in list(enumerate(PHASES)) + [(12, "fast precompute"), (13, "fast walk")]:
         print(f"  {name:24s} {100.0 * buf[k] / max(tot, 1):5.1f}%  {buf[k] / blocks:8.0f} cyc/block")
 
 
