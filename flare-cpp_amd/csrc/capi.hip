@@ -86,6 +86,7 @@ constexpr OptDesc kOptDesc[fsg::kOptCount] = {
     {"encode_wave_share", "FSG_ENCODE_WAVE_SHARE", 500},
     {"encode_wave_all_mb", "FSG_ENCODE_WAVE_ALL_MB", 640},
     {"encode_lanes", "FSG_ENCODE_LANES", 0},
+    {"encode_wave_per_cu", "FSG_ENCODE_WAVE_PER_CU", 0},
     {"lz4_big_min", "FSG_L4_BIG_MIN", -1},
 };
 std::atomic<int64_t> g_opt[fsg::kOptCount];

@@ -33,6 +33,7 @@ enum Opt : int {
   kOptEncodeWaveShare,    // wave encoder's share of long units (permille)
   kOptEncodeWaveAllMb,    // all long units to the wave encoder below this many MiB
   kOptEncodeLanes,        // lanes in flight of the lane encoder (0 = all)
+  kOptEncodeWavePerCu,    // wave encoder blocks per CU (0 = as many as LDS holds)
   // LZ4 two-pass decode (lz4_decode2.hip)
   kOptLz4BigMin,          // -1 automatic; blocks above this many bytes take the wave walk
   kOptCount

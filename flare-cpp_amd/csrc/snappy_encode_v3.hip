@@ -681,7 +681,9 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
   if (wave_min) {
     const u32 cap = max_in_len > kBlockSize ? kBlockSize : max_in_len;
     const u32 lds = table_size_for(cap) * 2;
-    const u32 per_cu = (160u * 1024u) / (lds + (u32)encode_wave_static_lds_bytes());
+    u32 per_cu = (160u * 1024u) / (lds + (u32)encode_wave_static_lds_bytes());
+    const i64 pc_opt = opt(kOptEncodeWavePerCu);
+    if (pc_opt > 0 && (u64)pc_opt < per_cu) per_cu = (u32)pc_opt;
     const u32 waves = 256u * (per_cu ? per_cu : 1u);
     hipStream_t wstream = stream;
     if (side) {

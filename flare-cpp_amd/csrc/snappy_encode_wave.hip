@@ -58,10 +58,15 @@ constexpr u32 kPredNone = 0xff, kPredUnknown = 0xfe;
 #endif
 // Output bytes stored straight to global memory (no LDS staging ring) and
 // the in-block predecessors found without a scratch array (see the pred
-// rounds), so the table is the wave's only LDS: five 32 KiB tables per CU
-// instead of four.  0 = the staging ring and the pred scratch (A/B builds).
+// rounds), so the table is the wave's only LDS (four 32 KiB tables stay
+// resident per CU either way; the gain is the ring's round trips).  0 = the
+// staging ring and the pred scratch (A/B builds).
 #ifndef FSG_WENC_DIRECT
 #define FSG_WENC_DIRECT 1
+#endif
+// Input loads two blocks ahead instead of one (A/B).
+#ifndef FSG_WENC_AHEAD2
+#define FSG_WENC_AHEAD2 0
 #endif
 // (ds_write_b8 into the staging ring, or a byte store to the output)
 #if FSG_WENC_DIRECT
@@ -354,6 +359,9 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
     u32 curB = 0xffffffffu;  // base of the block whose input is in xw
     W5 xw{}, xw1{}, xwp{};
     Raw20 xr2{};  // input of block curB + 128, in flight
+#if FSG_WENC_AHEAD2
+    Raw20 xr3{};  // and of block curB + 192 (input loads two blocks ahead)
+#endif
     u32 Tn = 0;
     Raw20 cbn{};
     bool spec = false, prev_ok = false;
@@ -367,16 +375,26 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       if (curB != 0xffffffffu && B == curB + 64) {
         xwp = xw;
         xw = xw1;
-        xw1 = shifted20(xr2);  // issued a block ago
+        xw1 = shifted20(xr2);  // issued a block ago (two with FSG_WENC_AHEAD2)
         prev_ok = true;
+#if FSG_WENC_AHEAD2
+        xr2 = xr3;
+        xr3 = raw20(fr, fal + B + 192 + lane);
+#endif
       } else {
         const Raw20 r0 = raw20(fr, fal + B + lane), r1 = raw20(fr, fal + B + 64 + lane);
+#if FSG_WENC_AHEAD2
+        xr2 = raw20(fr, fal + B + 128 + lane);
+        xr3 = raw20(fr, fal + B + 192 + lane);
+#endif
         xw = shifted20(r0);
         xw1 = shifted20(r1);
         spec = false;
         prev_ok = false;
       }
+#if !FSG_WENC_AHEAD2
       xr2 = raw20(fr, fal + B + 128 + lane);
+#endif
       curB = B;
       // the previous blocks' output, now that the waits above are behind us
       flush_to(pend_end);
