@@ -249,10 +249,23 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
   const size_t need = fsg::encode_tables_workspace_bytes(n_msgs, max_in_len, &slots);
   if ((forced == 0 || forced == 3) && d_workspace && workspace_bytes >= need) {
     const fsg::u32 cap = max_in_len == 0 || max_in_len > fsg::kBlockSize ? fsg::kBlockSize : max_in_len;
-    // Lanes in flight (tuning knob): fewer lanes keep their tables and
-    // recent input cache-resident; each lane then encodes more messages.
+    // Lanes in flight.  Beside the wave encoder (a batch with units long
+    // enough for it), 3/4 of the messages, at most 131,072: the lanes' waves
+    // share the SIMDs with the wave encoder's lone waves, whose serial chains
+    // set the batch's time, and fewer lanes keep their tables and recent
+    // input cache-resident, each encoding more messages.  Measured (A/B, one
+    // box): C5 27.0 -> 18.8 ms (131,072 of 262,144; 98,304: 20.8, 196,608:
+    // 22.4), C3 92.3 -> 85.4 ms (49,152 of 65,536; 32,768: 85.3).  Option
+    // encode_lanes overrides (0 = this rule).
     const unsigned lanes_cap = (unsigned)fsg::opt(fsg::kOptEncodeLanes);
-    if (lanes_cap && lanes_cap < slots) slots = (lanes_cap + 63) / 64 * 64;
+    const fsg::u32 wmin = encode_wave_min();
+    if (lanes_cap) {
+      if (lanes_cap < slots) slots = (lanes_cap + 63) / 64 * 64;
+    } else if (wmin && max_in_len >= wmin && n_msgs > 64) {
+      fsg::u32 beside = (fsg::u32)(((uint64_t)n_msgs * 3 / 4 + 255) / 256 * 256);
+      if (beside > 131072u) beside = 131072u;
+      if (beside < slots) slots = beside;
+    }
     return record(fsg::launch_encode_v3(d_in, d_in_off, d_in_len, n_msgs, max_in_len, d_out,
                                         d_out_off, d_out_len, d_status, d_workspace,
                                         workspace_bytes, slots, fsg::table_size_for(cap), need,

@@ -65,9 +65,13 @@ def main():
         kv = dict(x.split("=") for x in opts.split(",")) if opts else {}
         runs.append((spec, fsg.SnappyGPU(0, Path(path)), {k: int(v) for k, v in kv.items()}))
     res = {spec: [] for spec, _, _ in runs}
+    # specs sharing one library path share its option table: every turn
+    # starts from the values found at load time, then applies its own
+    touched = sorted({k for _, _, kv in runs for k in kv})
+    initial = {id(c.lib): {k: fsg.get_option(k, c.lib) for k in touched} for _, c, _ in runs}
     for r in range(args.rounds):
         for spec, codec, kv in runs:
-            for k, v in kv.items():
+            for k, v in {**initial[id(codec.lib)], **kv}.items():
                 fsg.set_option(k, v, codec.lib)
             step = lambda: codec.decompress(d_c, d_coff, d_cl, n, d_out, d_off, d_len, d_ol, d_st,  # noqa: E731
                                             stream=stream, workspace=dws)

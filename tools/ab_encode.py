@@ -63,10 +63,14 @@ def main():
         codec = fsg.SnappyGPU(0, Path(path))
         runs.append((spec, codec, kv, codec.compress_workspace(n, max_len)))
     res = {spec: [] for spec, _, _, _ in runs}
+    # specs sharing one library path share its option table: every turn
+    # starts from the values found at load time, then applies its own
+    touched = sorted({k for _, _, kv, _ in runs for k in kv})
+    initial = {id(c.lib): {k: fsg.get_option(k, c.lib) for k in touched} for _, c, _, _ in runs}
     ref_lens = None
     for r in range(args.rounds):
         for spec, codec, kv, ws in runs:
-            for k, v in kv.items():
+            for k, v in {**initial[id(codec.lib)], **kv}.items():
                 fsg.set_option(k, v, codec.lib)
             step = lambda: codec.compress(d_raw, d_off, d_len, n, max_len, d_c, d_coff, d_cl, d_st,  # noqa: E731
                                           stream=stream, workspace=ws)
