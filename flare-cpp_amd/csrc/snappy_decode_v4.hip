@@ -1579,6 +1579,10 @@ namespace {
 #ifndef FSG_PF_POS
 #define FSG_PF_POS 0
 #endif
+// The software-pipelined execution pass (exec6_message; A/B variant).
+#ifndef FSG_EXEC_PIPE
+#define FSG_EXEC_PIPE 0
+#endif
 // Window and kept history: 3 KiB / 1 KiB at 7 waves per SIMD (C3 6.35 ->
 // 6.20 ms against 4 KiB / 2 KiB at 6 waves, A/B on one box; 4 KiB / 1 KiB
 // at 6 waves 6.33, a 256-entry tag ring 7.04).
@@ -2528,6 +2532,382 @@ __device__ __forceinline__ void exec5_message(
 #endif
 }
 
+#if FSG_EXEC_PIPE
+// ===========================================================================
+// Software-pipelined execution pass (A/B variant, -DFSG_EXEC_PIPE=1; VERDICT
+// r4 item 1): the same group rules as exec5_message, but the NEXT group's
+// front -- ring read, tag decode, prefix sum, writer checks, chunk
+// classification, round-A loads, the prefetch of the group after it and the
+// window zeroing -- is issued before this group's rounds B, so its loads are
+// in flight while the rounds run.  The early front is taken only when it
+// needs no ring refill, no window slide and no long literal (else the group
+// goes the ordinary way), and it treats only output below this group's first
+// byte as final (its near-ready chunks: bytes this group's rounds B have not
+// written yet wait for its own rounds B).  Far loads stay safe: every far
+// source lies below the window base, which the last slide flushed and waited
+// for (section 4, "far copies").
+// ===========================================================================
+__device__ __forceinline__ void exec6_message(
+    u32 m, const u8* __restrict__ in, const u64* __restrict__ in_off,
+    const u32* __restrict__ in_len, u8* out, const u64* __restrict__ out_off,
+    const u32* __restrict__ out_len, i32* __restrict__ status, const u32* __restrict__ bm_base,
+    const u32* __restrict__ bitmap, u32* ring, const u32* tagtab, u8* sb, const u32x4* sel_tab,
+    const u32x4* mtab, u32 lane, i32 st, u32 ip0, u32 op0, u32 op1, bool prio, u32 keep_hist) {
+  const u32 bmb = bm_base[m];
+  const u32 n_in = in_len[m];
+  const u32 expected = out_len[m];
+  const u8* ib = in + in_off[m];
+  u8* ob = out + out_off[m];
+  if (st != kOk) return;
+  const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
+  const u32 obal = (u32)(reinterpret_cast<uintptr_t>(ob) & 15);
+  const __amdgpu_buffer_rsrc_t irsrc = msg_rsrc(ib - ibal, ibal + n_in);
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc(ob - obal, (short)0, (int)(expected + obal), 0x00020000);
+
+  if ((bmb & kSingleLiteral) && op1 == expected && op0 == 0) {
+    const u32 S = bmb & ~kSingleLiteral;
+    for (u32 k0 = 0; k0 < expected; k0 += 4096) {
+      Raw16 x[4];
+#pragma unroll
+      for (u32 r = 0; r < 4; ++r) x[r] = raw_load16(irsrc, S + k0 + 1024 * r + lane * 16 + ibal);
+#pragma unroll
+      for (u32 r = 0; r < 4; ++r) {
+        const u32 k = k0 + 1024 * r + lane * 16;
+        if (k < expected) store_exact(ob + k, shifted16(x[r]), expected - k < 16 ? expected - k : 16u);
+      }
+    }
+    return;
+  }
+  const u32* bm = bitmap + bmb;
+  const u32 nwords = (n_in + 31) >> 5;
+
+  u32 head = 0, tail = 0, scan = ip0 >> 5, op = op0;
+  int sbase = (int)((op0 + obal) & ~15u) - (int)obal;
+  u32 flushed = op0;
+  auto zero_from = [&](u32 from) {
+    const u32 i = from + 16 * lane;
+    if (i < kWindow + 32) *reinterpret_cast<u32x4*>(sb + i) = u32x4{0, 0, 0, 0};
+  };
+  zero_from(0);
+  u32 zero_end = 1024;
+  wave_lds_fence();
+  auto fill_word = [&](u32 sc) -> u32 {
+    const u32 wi = sc + (lane >> 2);
+    return (lane < 4 * kFillWords && wi < nwords) ? bm[wi] : 0u;
+  };
+  u32 bmw = fill_word(scan);
+  u32 pf_head = 0xffffffffu, pf_cnt = 0;
+  u32x4 pd = u32x4{0, 0, 0, 0};
+  u32 pd4 = 0;
+  auto prefetch = [&](u32 p) {
+    const u32 a = (p + ibal) & ~3u;
+    pd = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
+    pd4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
+  };
+  auto flush_to = [&](u32 fe) {
+    if (fe <= flushed) return;
+    const int b0 = (int)(((flushed + obal) & ~15u)) - (int)obal;
+    for (int blk = b0 + 16 * (int)lane; blk < (int)fe; blk += 1024) {
+      const u32 lo = blk < (int)flushed ? flushed : (u32)blk;
+      const u32 hi = blk + 16 < (int)fe ? (u32)(blk + 16) : fe;
+      if (hi - lo == 16) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(sb + (blk - sbase));
+        __builtin_memcpy(ob + blk, &v, 16);
+      } else {
+        store_exact(ob + lo, lds_read16(sb + ((int)lo - sbase)), hi - lo);
+      }
+    }
+    flushed = fe;
+  };
+
+  // ---- the group state, loop-carried: the front of the group at `head`
+  // (decoded, scanned, classified, round-A loads in flight) when `have`
+  bool have = false;
+  u32 len = 0, off = 0, src = 0, t_op = 0, kf = 0, sh = 0, kfar = 0, k_tags = 0, tot_len = 0, lsrc = 0;
+  bool is_lit = false, reg0 = false, pat = false, fits = false;
+  u64 m1 = 0;
+  u32x4 a0 = u32x4{0, 0, 0, 0}, a1 = u32x4{0, 0, 0, 0};
+  u32 a0e = 0, a1e = 0;
+  auto gload = [&](u32 k, u32x4& d, u32& d4) {
+    if (is_lit) {
+      const u32 a = (src + 16 * k + ibal) & ~3u;
+      d = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
+      d4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
+    } else if (k >= kfar) {
+      d = lds_read16(sb + ((int)(src + 16 * k) - sbase));
+    } else {
+      d = far_load(orsrc, src + 16 * k + obal);
+    }
+  };
+  // The front of the group at ghead whose first output byte is gop; output
+  // below `ready` is final.  Early: no slide, and the prefetch must be this
+  // group's.  Returns 0 done, 1 a long literal first (nothing changed), 2 a
+  // slide needed (early only), 3 corrupt (status written), 4 no prefetch.
+  auto front = [&](u32 ghead, u32 gop, u32 ready, bool early) -> int {
+    const u32 avail = tail - ghead;
+    const u32 take0 = avail < 64 ? avail : 64u;
+    const bool valid = lane < take0;
+    const bool pf_ok = pf_head == ghead && pf_cnt >= take0;
+    if (early && !pf_ok) return 4;
+    const u32 pos = ring[(ghead + lane) & (kTagRing - 1)];
+    if (!pf_ok) prefetch(pos);
+    if (prio) __builtin_amdgcn_s_setprio(1);
+    const u32 s = (pos + ibal) & 3u;
+    const u32 c = __builtin_amdgcn_alignbyte(pd[1], pd[0], s) & 0xffu;
+    const u32 e = tagtab[c];
+    const bool q = s == 3;
+    const u32 w0 = q ? pd[1] : pd[0], w1 = q ? pd[2] : pd[1], w2 = q ? pd[3] : pd[2];
+    const u32 w3 = q ? pd4 : pd[3];
+    const u32 b = (s + 1) & 3u;
+    const u32x4 xr = u32x4{__builtin_amdgcn_alignbyte(w1, w0, b), __builtin_amdgcn_alignbyte(w2, w1, b),
+                           __builtin_amdgcn_alignbyte(w3, w2, b), __builtin_amdgcn_alignbyte(pd4, w3, b)};
+    const u32 val = xr[0] & (0xffffffffu >> (e & 31u));
+    const bool lit = e & 64u;
+    const u32 ln = (e & 32u) ? val + 1u : (e >> 8) & 0x7fu;
+    const u32 nb = (e >> 16) & 7u;
+    const u64 bigm = __ballot(valid && lit && ln > 64);
+    if (bigm & 1ull) {
+      len = ln;
+      lsrc = pos + 1 + nb;
+      return 1;
+    }
+    is_lit = lit;
+    len = ln;
+    off = val + (e >> 20);
+    lsrc = pos + 1 + nb;
+    const u32 take = bigm ? (u32)__builtin_ctzll(bigm) : take0;
+    const bool v = lane < take;
+    const u32 lv = v ? len : 0u;
+    const u32 incl = dpp_incl_scan(lv);
+    t_op = gop + incl - lv;
+    fits = v && incl <= kGroupBytes && t_op < op1;
+    k_tags = (u32)__builtin_popcountll(__ballot(fits));
+    tot_len = readlane(incl, k_tags - 1);
+    if (__any(fits && (len > op1 - t_op || (!is_lit && (off == 0 || off > t_op - op0))))) {
+      if (lane == 0) status[m] = kCorrupt;
+      return 3;
+    }
+    if (gop + tot_len - sbase > kWindow) {
+      if (early) return 2;
+      const int nsb = (int)(((gop - keep_hist + obal) & ~15u)) - (int)obal;
+      if ((int)flushed < nsb + 16) flush_to((u32)((int)((gop + obal) & ~15u) - (int)obal));
+      wait_all_memory();
+      const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)gop - nsb);
+      for (u32 k = 0; k < keep; k += 1024) {
+        const u32 i = k + 16 * lane;
+        u32x4 x = u32x4{0, 0, 0, 0};
+        if (i < keep) x = *reinterpret_cast<const u32x4*>(sb + shift + i);
+        wave_lds_fence();
+        if (i < keep) *reinterpret_cast<u32x4*>(sb + i) = x;
+        wave_lds_fence();
+      }
+      sbase = nsb;
+      zero_end = (keep + 15) & ~15u;
+    }
+    src = is_lit ? lsrc : t_op - off;
+    const u32 nch = (len + 15) >> 4;
+    pat = !is_lit && off < 16 && off < len;
+    const u32 below = (u32)(sbase - (int)src);
+    kfar = (int)below > 0 ? ((below - 1) >> 4) + 1 : 0u;
+    const u32 kready = src + len <= ready ? nch : (src < ready ? (ready - src) >> 4 : 0u);
+    const u32 klead = kfar > kready ? kfar : kready;
+    const u32 kc = pat ? 0u : (klead < nch ? klead : nch);
+    kf = fits ? (is_lit ? nch : kc) : 0u;
+    reg0 = is_lit && nb == 0;
+    sh = is_lit ? (src + ibal) & 3u : 0u;
+    a0 = xr;
+    a1 = u32x4{0, 0, 0, 0};
+    a0e = 0;
+    a1e = 0;
+    if (kf > 0 && !reg0) gload(0, a0, a0e);
+    m1 = __ballot(kf > 1);
+    if (m1 && kf > 1) gload(1, a1, a1e);
+    {  // the next group's tag bytes; the window zeroed ahead
+      const u32 nh = ghead + k_tags;
+      const u32 na = tail - nh;
+      pf_head = nh;
+      pf_cnt = na < 64 ? na : 64u;
+      prefetch(ring[(nh + lane) & (kTagRing - 1)]);
+      while (gop + tot_len + 20 - sbase > zero_end) {
+        zero_from(zero_end);
+        zero_end += 1024;
+      }
+      wave_lds_fence();
+    }
+    if (prio) __builtin_amdgcn_s_setprio(0);
+    return 0;
+  };
+  auto shf = [&](const u32x4& d, u32 d4, u32 t) {
+    return u32x4{__builtin_amdgcn_alignbyte(d[1], d[0], t), __builtin_amdgcn_alignbyte(d[2], d[1], t),
+                 __builtin_amdgcn_alignbyte(d[3], d[2], t), __builtin_amdgcn_alignbyte(d4, d[3], t)};
+  };
+
+  for (;;) {
+    if (!have) {
+      if (tail - head < 2 * kMaxPieces && scan < nwords) {
+        if (prio) __builtin_amdgcn_s_setprio(1);
+        u32 bits = (bmw >> (8 * (lane & 3))) & 0xffu;
+        const u32 bitbase = (scan + (lane >> 2)) * 32 + 8 * (lane & 3);
+        if (bitbase < ip0) bits &= bitbase + 8 <= ip0 ? 0u : (0xffu << (ip0 - bitbase)) & 0xffu;
+        const u32 cnt = __builtin_popcount(bits);
+        const u32 incl = dpp_incl_scan(cnt);
+        u32 slot = tail + incl - cnt;
+        while (bits) {
+          ring[slot & (kTagRing - 1)] = bitbase + __builtin_ctz(bits);
+          ++slot;
+          bits &= bits - 1;
+        }
+        tail += readlane(incl, 63);
+        scan += kFillWords;
+        bmw = fill_word(scan);
+        wave_lds_fence();
+        continue;
+      }
+      if (tail == head || op >= op1) break;
+      const int r = front(head, op, op, false);
+      if (r == 3) return;
+      if (r == 1) {
+        // ---------- long literal: written straight to the slot by the
+        // whole wave; the window restarts behind it (as exec5_message)
+        const u32 L = readlane(len, 0), S = readlane(lsrc, 0);
+        if ((u64)op + L > op1) {
+          if (lane == 0) status[m] = kCorrupt;
+          return;
+        }
+        flush_to(op);
+        for (u32 k0 = 0; k0 < L; k0 += 4096) {
+          Raw16 x[4];
+#pragma unroll
+          for (u32 r2 = 0; r2 < 4; ++r2) x[r2] = raw_load16(irsrc, S + k0 + 1024 * r2 + lane * 16 + ibal);
+#pragma unroll
+          for (u32 r2 = 0; r2 < 4; ++r2) {
+            const u32 k = k0 + 1024 * r2 + lane * 16;
+            if (k < L) store_exact(ob + op + k, shifted16(x[r2]), L - k < 16 ? L - k : 16u);
+          }
+        }
+        op += L;
+        flushed = op;
+        sbase = (int)((op + obal) & ~15u) - (int)obal - 16;
+        zero_from(0);
+        zero_end = 1024;
+        wave_lds_fence();
+        if (lane < 2) {
+          const u32 lo = (u32)sbase + 16 * lane;
+          if (lo < op) {
+            const u32 cnt = op - lo < 16 ? op - lo : 16u;
+            store_exact(sb + 16 * lane, rsrc_load16(irsrc, S + L - (op - lo) + ibal), cnt);
+          }
+        }
+        wave_lds_fence();
+        head += 1;
+        pf_head = 0xffffffffu;
+        if (head == tail) {
+          const u32 nw = (S + L) >> 5;
+          if (nw > scan) {
+            scan = nw;
+            bmw = fill_word(scan);
+          }
+        }
+        continue;
+      }
+    }
+    have = false;
+    {  // the previous groups' completed blocks, while the loads are in flight
+      const int fe = (int)((op + obal) & ~15u) - (int)obal;
+      if (fe >= (int)flushed + 1024) flush_to((u32)fe);
+    }
+    const u32 wa = (u32)((int)t_op - sbase);
+    if (kf > 0) or_store(sb, wa, shf(a0, a0e, reg0 ? 0u : sh), len < 16 ? len : 16u, mtab);
+    if (m1) {
+      if (kf > 1) or_store(sb, wa + 16, shf(a1, a1e, sh), len - 16 < 16 ? len - 16 : 16u, mtab);
+      if (__ballot(kf > 2)) {
+        if (kf > 2) gload(2, a0, a0e);
+        if (kf > 3) gload(3, a1, a1e);
+        if (kf > 2) or_store(sb, wa + 32, shf(a0, a0e, sh), len - 32 < 16 ? len - 32 : 16u, mtab);
+        if (kf > 3) or_store(sb, wa + 48, shf(a1, a1e, sh), len - 48, mtab);
+      }
+    }
+    wave_lds_fence();
+    // ---------- rounds B state of this group (as exec5_message)
+    u32 rem = (fits && kf < ((len + 15) >> 4)) ? len - 16 * kf : 0u;
+    u32 cw = (u32)((int)t_op - sbase) + 16 * kf;
+    u32 sw = (u32)((int)src - sbase) + 16 * kf;
+    const bool gpat = pat;
+    const u32 goff = off;
+    const u32 stp = gpat ? pat_step(goff) : 16u;
+    u32 n = rem < stp ? rem : stp;
+    bool pf = gpat;
+    u32 ne = rem ? (pf ? cw : sw + n) : 0xffffffffu;
+    u64 pend = __ballot(rem > 0);
+    const u32 g_tot = tot_len, g_k = k_tags;
+    // ---------- the next group's front, before this group's rounds B
+    {
+      const u32 nh = head + g_k, nop = op + g_tot;
+      if ((tail - nh >= 2 * kMaxPieces || scan >= nwords) && tail > nh && nop < op1) {
+        const int r = front(nh, nop, op, true);
+        if (r == 3) return;
+        have = r == 0;
+      }
+    }
+    // ---------- rounds B (as exec5_message)
+    if (!__ballot(gpat && rem > 0)) {
+      while (pend) {
+        const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
+        if (ne <= W) {
+          const u32x4 x = lds_read16(sb + sw);
+          const u32x4 o = lds_read16(sb + cw);
+          const u32x4 mk = mtab[n];
+          u32x4 y;
+          y[0] = (x[0] & mk[0]) | (o[0] & ~mk[0]);
+          y[1] = (x[1] & mk[1]) | (o[1] & ~mk[1]);
+          y[2] = (x[2] & mk[2]) | (o[2] & ~mk[2]);
+          y[3] = (x[3] & mk[3]) | (o[3] & ~mk[3]);
+          __builtin_memcpy(sb + cw, &y, 16);
+          rem -= n;
+          cw += n;
+          sw += n;
+          n = rem < 16u ? rem : 16u;
+          ne = rem ? sw + n : 0xffffffffu;
+        }
+        wave_lds_fence();
+        pend = __ballot(rem > 0);
+      }
+    }
+    while (pend) {
+      const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
+      if (ne <= W) {
+        u32x4 x = lds_read16(sb + sw);
+        if (pf) x = expand_pattern(x, goff, sel_tab);
+        const u32x4 o = lds_read16(sb + cw);
+        const u32x4 mk = mtab[n];
+        u32x4 y;
+        y[0] = (x[0] & mk[0]) | (o[0] & ~mk[0]);
+        y[1] = (x[1] & mk[1]) | (o[1] & ~mk[1]);
+        y[2] = (x[2] & mk[2]) | (o[2] & ~mk[2]);
+        y[3] = (x[3] & mk[3]) | (o[3] & ~mk[3]);
+        __builtin_memcpy(sb + cw, &y, 16);
+        rem -= n;
+        cw += n;
+        sw = gpat ? cw - stp : sw + n;
+        pf = false;
+        n = rem < stp ? rem : stp;
+        ne = rem ? sw + n : 0xffffffffu;
+      }
+      wave_lds_fence();
+      pend = __ballot(rem > 0);
+    }
+    op += g_tot;
+    head += g_k;
+  }
+  if (op != op1) {  // the stream ended early (snappy.cc:858-868)
+    if (lane == 0) status[m] = kCorrupt;
+    return;
+  }
+  flush_to(op1);
+}
+#endif
+
 // 7 waves per SIMD by default (FSG_EXEC_WAVES; 72 VGPRs, 22.2 KB of LDS per
 // block with the 3 KiB window: C3 6.35 -> 6.20 ms against 6 waves with a
 // 4 KiB window, A/B on one box; 8 waves spill and were slower).
@@ -2566,8 +2946,13 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
   // one message (or segment) with the pass-2 variant V
   auto run = [&](u32 m, u32* ring, u8* pmap, u8* sb, u32 lane, i32 st, u32 ip0, u32 op0, u32 op1) {
     if constexpr (V == 5)
+#if FSG_EXEC_PIPE
+      exec6_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, tagtab,
+                    sb, sel_tab, mask_tab, lane, st, ip0, op0, op1, prio != 0, keep_hist);
+#else
       exec5_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, tagtab,
                     sb, sel_tab, mask_tab, lane, st, ip0, op0, op1, prio != 0, keep_hist);
+#endif
     else
       exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, pmap,
                    sb, sel_tab, mask_tab, lane, st, ip0, op0, op1, prio != 0, keep_hist);

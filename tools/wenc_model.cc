@@ -30,7 +30,7 @@ static inline u32 hashb(u32 x, int shift) { return (x * kHashMul) >> shift; }
 
 struct Stats {
   u64 blocks = 0, events = 0, probes = 0, pred_rounds = 0, deep = 0, slow_resolve = 0, long_match = 0,
-      jumps = 0, direct_inserts = 0, frags = 0, fast = 0;
+      jumps = 0, direct_inserts = 0, frags = 0, fast = 0, why[6] = {0, 0, 0, 0, 0, 0};
 } st;
 static int g_trace = 0;
 
@@ -198,9 +198,11 @@ static u8* wenc_fragment(const u8* f, u32 n, u8* op, u16* table, u32 ht) {
         bool found = false;
         // would the kernel's fast event path (FSG_WENC_FAST) take this event?
         bool fast_ok = mode == POST;
+        int why = mode == POST ? -1 : 0;  // first reason the fast path would not take it
         const u32 ip_at = ip;
         if (mode == POST) {
           const int k0 = (int)(ip - B);
+          if (fast_ok && pred1[k0] != -1 && why < 0) why = 1;
           fast_ok = fast_ok && pred1[k0] == -1;
           cand = resolve(k0, I);
           I |= 1ull << k0;
@@ -222,6 +224,8 @@ static u8* wenc_fragment(const u8* f, u32 n, u8* op, u16* table, u32 ht) {
             const u32 step = sk >> 5;
             if (p + step > lim) { done = true; break; }
             const int k = (int)(p - B);
+            if (fast_ok && pred1[k] != -1 && why < 0) why = 2;
+            if (fast_ok && !(p - ip_at <= 32 && sk < 64) && why < 0) why = 3;
             fast_ok = fast_ok && pred1[k] == -1 && p - ip_at <= 32 && sk < 64;
             cand = resolve(k, I);
             I |= 1ull << k;
@@ -247,6 +251,7 @@ static u8* wenc_fragment(const u8* f, u32 n, u8* op, u16* table, u32 ht) {
         while (q + m < n && f[cand + m] == f[q + m]) ++m;
         if (m > 20) st.long_match++;
         if (fast_ok && (m < 20 || q + 20 >= n)) st.fast++;
+        else st.why[why >= 0 ? why : 4]++;
         if (g_trace) printf("copy %u %u %u\n", q, cand, m);
         op = emit_copy(op, q - cand, m);
         ip = q + m;
@@ -375,7 +380,10 @@ int main(int argc, char** argv) {
     dg_text_body(t * 257, x.data(), x.size());
     wenc_compress(x.data(), x.size(), o.data());
   }
-  printf("C3 fast-path events %.1f%%\n", 100.0 * st.fast / st.events);
+  printf("C3 fast-path events %.1f%%; others per block: not post %.3f, pred at ip %.3f, pred in search %.3f, "
+         "search past 32 %.3f, long match %.3f\n", 100.0 * st.fast / st.events, (double)st.why[0] / st.blocks,
+         (double)st.why[1] / st.blocks, (double)st.why[2] / st.blocks, (double)st.why[3] / st.blocks,
+         (double)st.why[4] / st.blocks);
   {
     Stats c3 = st;
     st = Stats();
