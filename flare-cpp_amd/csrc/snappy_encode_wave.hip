@@ -64,6 +64,12 @@ constexpr u32 kPredNone = 0xff, kPredUnknown = 0xfe;
 #ifndef FSG_WENC_DIRECT
 #define FSG_WENC_DIRECT 1
 #endif
+// With FSG_WENC_FAST 2: the fast events' chains resolved for every lane at
+// once by pointer doubling after the precomputation, so an arrival takes its
+// whole chain in a few readlanes; 0 = the walk, one readlane chain per event.
+#ifndef FSG_WENC_CHAIN
+#define FSG_WENC_CHAIN 0
+#endif
 // Input loads two blocks ahead instead of one (A/B).
 #ifndef FSG_WENC_AHEAD2
 #define FSG_WENC_AHEAD2 0
@@ -608,6 +614,39 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
         fECM = (fpk & 0xffffu) | (fml << 16);
         FastM = __ballot(((Stat >> k) & 1ull) && (hit || miss_ok) && !lng);
       }
+#if FSG_WENC_CHAIN
+      // The walk below, for every arrival lane at once: lane k's chain is k,
+      // then its successor's lane while that lane is fast and its position
+      // lies below min(lim, B + 64).  Pointer doubling over the successor
+      // lanes: after round r, cm = the chain's first 2^r lanes, ci = their
+      // inserts, cn = where they leave.  A fast event advances >= 4
+      // positions (a 4-byte match), so a chain has <= 16 lanes: 4 rounds.
+      u32 cmlo, cmhi, cilo, cihi, cn;
+      {
+        const u32 stop = lim < B + 64 ? lim : B + 64;
+        const u32 nl = fsucc - B;
+        u32 J = (((FastM >> lane) & 1ull) && fsucc < stop && ((FastM >> (nl & 63)) & 1ull)) ? nl : 64u;
+        cmlo = lane < 32 ? 1u << lane : 0u;
+        cmhi = lane < 32 ? 0u : 1u << (lane - 32);
+        cilo = filo;
+        cihi = fihi;
+        cn = fsucc;
+        for (int r = 0; r < 4; ++r) {
+          if (!__ballot(J < 64)) break;
+          const u32 src = J < 64 ? J : lane;
+          const u32 jj = bperm(J, src), ml = bperm(cmlo, src), mh = bperm(cmhi, src);
+          const u32 il = bperm(cilo, src), ih = bperm(cihi, src), nj = bperm(cn, src);
+          if (J < 64) {
+            cmlo |= ml;
+            cmhi |= mh;
+            cilo |= il;
+            cihi |= ih;
+            cn = nj;
+            J = jj;
+          }
+        }
+      }
+#endif
       STAMP(12);
 #endif
       bool done = false, leave = false;
@@ -617,6 +656,12 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
         // over the lanes' successors while the arrival lane's event is fast,
         // up to the first arrival past the block or the input limit
         if (post && ((FastM >> (ip - B)) & 1ull)) {
+#if FSG_WENC_CHAIN
+          const u32 k0 = ip - B;
+          const u32 nip = rl(cn, k0);
+          const u64 evs = ((u64)rl(cmhi, k0) << 32) | (u64)rl(cmlo, k0);
+          const u64 iadd = ((u64)rl(cihi, k0) << 32) | (u64)rl(cilo, k0);
+#else
           const u32 stop = lim < B + 64 ? lim : B + 64;
           u32 k0 = ip - B, nip;
           u64 evs = 0, iadd = 0;
@@ -628,6 +673,7 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
             k0 = nip - B;
             if (!((FastM >> k0) & 1ull)) break;
           }
+#endif
           I |= iadd;
           EvM |= evs;
           FastEv |= evs;
