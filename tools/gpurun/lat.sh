@@ -2,7 +2,7 @@
 # Item 5: account for one single-message device batch.  The echo
 # bench with every body on the GPU, under the kernel + HIP API trace.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/lat
+O=${OUT:-gpurun_out/lat}
 rm -rf $O; mkdir -p $O
 timeout -k 10 120 build/echo_bench --codec gpu --calls ${CALLS:-200} > $O/echo_gpu.json 2> $O/echo_gpu.err || { tail -5 $O/echo_gpu.err; exit 1; }
 cat $O/echo_gpu.json | head -c 1500; echo
