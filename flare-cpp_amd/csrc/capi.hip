@@ -40,6 +40,12 @@ hipError_t launch_encode(const u8* in, const u64* in_off, const u32* in_len,
                          u32* out_len, i32* status, hipStream_t stream);
 hipError_t launch_gather_blocks(const u64* src, const u32* len, const u64* dst_off, u32 n, u8* dst,
                                 hipStream_t stream);
+hipError_t launch_decode_partial(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u32 frag,
+                                 u8* out, const u64* out_off, const u32* out_cap, u32* got, u64* produced,
+                                 i32* status, hipStream_t stream);
+hipError_t launch_iov_scatter(const u8* stage, const u64* stage_off, const u32* out_len, u32 n_msgs,
+                              const u64* iov_base, const u64* iov_len, const u32* iov_first, i32* status,
+                              hipStream_t stream);
 size_t lz4_compress_workspace_bytes(u32 n_msgs);
 hipError_t launch_lz4_encode(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u8* out,
                              const u64* out_off, u32* out_len, i32* status, void* ws, hipStream_t stream);
@@ -359,6 +365,39 @@ int decompress_impl(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_
 }  // namespace
 
 extern "C" {
+
+int fsg_decompress_batch_partial(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                                 uint32_t n_msgs, uint32_t frag, uint8_t* d_out, const uint64_t* d_out_off,
+                                 const uint32_t* d_out_cap, uint32_t* d_got, uint64_t* d_produced,
+                                 int32_t* d_status, void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_cap || !d_got ||
+                 !d_produced || !d_status))
+    return FSG_ERR_INVALID_ARG;
+  // the batch decoder (lenient header, as the Source path reads it), then the
+  // streams it rejected through the scattered-writer model
+  const int r = decompress_impl(d_in, d_in_off, d_in_len, n_msgs, d_out, d_out_off, d_out_cap, d_got, d_status,
+                                0u, d_workspace, workspace_bytes, stream, nullptr);
+  if (r != FSG_SUCCESS) return r;
+  return record(fsg::launch_decode_partial(d_in, d_in_off, d_in_len, n_msgs, frag, d_out, d_out_off, d_out_cap,
+                                           d_got, d_produced, d_status, (hipStream_t)stream),
+                "fsg_decompress_batch_partial");
+}
+
+int fsg_decompress_batch_iovec(const uint8_t* d_in, const uint64_t* d_in_off, const uint32_t* d_in_len,
+                               uint32_t n_msgs, const uint64_t* d_iov_base, const uint64_t* d_iov_len,
+                               const uint32_t* d_iov_first, uint8_t* d_stage, const uint64_t* d_stage_off,
+                               const uint32_t* d_stage_cap, uint32_t* d_out_len, int32_t* d_status,
+                               void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (n_msgs && (!d_in || !d_in_off || !d_in_len || !d_iov_base || !d_iov_len || !d_iov_first || !d_stage ||
+                 !d_stage_off || !d_stage_cap || !d_out_len || !d_status))
+    return FSG_ERR_INVALID_ARG;
+  const int r = decompress_impl(d_in, d_in_off, d_in_len, n_msgs, d_stage, d_stage_off, d_stage_cap, d_out_len,
+                                d_status, 0u, d_workspace, workspace_bytes, stream, nullptr);
+  if (r != FSG_SUCCESS) return r;
+  return record(fsg::launch_iov_scatter(d_stage, d_stage_off, d_out_len, n_msgs, d_iov_base, d_iov_len, d_iov_first,
+                                        d_status, (hipStream_t)stream),
+                "fsg_decompress_batch_iovec");
+}
 
 // ---- LZ4 (include/flare_lz4_gpu.h)
 size_t fsg_lz4_max_compressed_length(size_t n) { return 5 + n + n / 255 + 16; }

@@ -19,7 +19,7 @@ REPO_DIR = PKG_DIR.parent
 HEADER = REPO_DIR / "include" / "flare_snappy_gpu.h"
 HEADERS = (HEADER, REPO_DIR / "include" / "flare_lz4_gpu.h")
 
-FSG_OK, FSG_CORRUPT, FSG_BAD_HEADER, FSG_SLOT_TOO_SMALL = 0, 1, 2, 3
+FSG_OK, FSG_CORRUPT, FSG_BAD_HEADER, FSG_SLOT_TOO_SMALL, FSG_IOV_TOO_SMALL = 0, 1, 2, 3, 4
 FSG_FLAG_VALIDATE_ONLY, FSG_FLAG_STRICT_HEADER = 1, 2
 
 _c = ctypes
@@ -43,6 +43,10 @@ _SIGS = {
     "fsg_decompress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
     "fsg_decompress_batch_2s": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp,
                                            _vp]),
+    "fsg_decompress_batch_partial": (_c.c_int, [_vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                _sz, _vp]),
+    "fsg_decompress_batch_iovec": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                              _sz, _vp]),
     "fsg_lz4_max_compressed_length": (_sz, [_sz]),
     "fsg_lz4_compress_workspace_bytes": (_sz, [_u32]),
     "fsg_lz4_compress_batch": (_c.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
@@ -63,7 +67,7 @@ def header_symbols(header: Path | None = None) -> list[str]:
 
 
 # entry points an older library under A/B may lack
-_OPTIONAL = {"fsg_decompress_batch_2s", "fsg_lz4_decompress_batch_2s", "fsg_lz4_decompress_batch_ws",
+_OPTIONAL = {"fsg_decompress_batch_2s", "fsg_decompress_batch_partial", "fsg_decompress_batch_iovec", "fsg_lz4_decompress_batch_2s", "fsg_lz4_decompress_batch_ws",
              "fsg_lz4_decompress_workspace_bytes", "fsg_set_option", "fsg_get_option", "fsg_default_option"}
 
 
@@ -184,6 +188,26 @@ class SnappyGPU:
         else:
             self._check(self.lib.fsg_decompress_batch_2s(*args, self._stream(pass1_stream)),
                         "fsg_decompress_batch_2s")
+
+    def decompress_partial(self, d_in, d_in_off, d_in_len, n, frag, d_out, d_out_off, d_out_cap, d_got,
+                           d_produced, d_status, stream=None, workspace=None):
+        """fsg_decompress_batch_partial: UncompressAsMuchAsPossible per message
+        (d_produced int64 / uint64, d_got int32 / uint32)."""
+        ws = 0 if workspace is None else workspace.numel() * workspace.element_size()
+        self._check(self.lib.fsg_decompress_batch_partial(
+            _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, frag, _ptr(d_out), _ptr(d_out_off), _ptr(d_out_cap),
+            _ptr(d_got), _ptr(d_produced), _ptr(d_status), _ptr(workspace), ws, self._stream(stream)),
+            "fsg_decompress_batch_partial")
+
+    def decompress_iovec(self, d_in, d_in_off, d_in_len, n, d_iov_base, d_iov_len, d_iov_first, d_stage,
+                         d_stage_off, d_stage_cap, d_out_len, d_status, stream=None, workspace=None):
+        """fsg_decompress_batch_iovec: RawUncompressToIOVec per message (d_iov_base:
+        int64 device addresses, d_iov_len int64, d_iov_first int32 with n + 1 entries)."""
+        ws = 0 if workspace is None else workspace.numel() * workspace.element_size()
+        self._check(self.lib.fsg_decompress_batch_iovec(
+            _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), n, _ptr(d_iov_base), _ptr(d_iov_len), _ptr(d_iov_first),
+            _ptr(d_stage), _ptr(d_stage_off), _ptr(d_stage_cap), _ptr(d_out_len), _ptr(d_status), _ptr(workspace),
+            ws, self._stream(stream)), "fsg_decompress_batch_iovec")
 
     # ---- LZ4 (include/flare_lz4_gpu.h)
     def lz4_compress_workspace(self, n, device=None):

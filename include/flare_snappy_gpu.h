@@ -22,6 +22,14 @@
  *                                  with FSG_FLAG_STRICT_HEADER it is the flat
  *                                  Uncompress(const char*, size_t, string*)
  *                                  (snappy.cc:1239-1251).
+ *   fsg_decompress_batch_partial   snappy.cc:1530-1535
+ *                                  (snappy::UncompressAsMuchAsPossible(
+ *                                  Source*, Sink*), SnappyScatteredWriter
+ *                                  :1331-1481)
+ *   fsg_decompress_batch_iovec     snappy.cc:1122-1132
+ *                                  (snappy::RawUncompressToIOVec(const char*,
+ *                                  size_t, const iovec*, size_t),
+ *                                  SnappyIOVecWriter :963-1120)
  *
  * Conventions: plain C, no exceptions, no torch types.  All buffers passed
  * to *_batch functions are DEVICE pointers (hipMalloc'd or device-mapped
@@ -40,6 +48,9 @@
  *   FSG_SLOT_TOO_SMALL  caller sizing error: the header's uncompressed length
  *                       exceeds the output slot (not a reference verdict;
  *                       size slots with fsg_get_uncompressed_length).
+ *   FSG_IOV_TOO_SMALL   (fsg_decompress_batch_iovec) the stream is valid but
+ *                       its iovecs hold fewer bytes than the header's length:
+ *                       the reference returns false.
  * On any status other than FSG_OK the content of the output slot is
  * unspecified (the reference's partial output on failure depends on the
  * source fragmentation, snappy.cc:866, and every caller discards it).
@@ -58,6 +69,7 @@ extern "C" {
 #define FSG_CORRUPT 1
 #define FSG_BAD_HEADER 2
 #define FSG_SLOT_TOO_SMALL 3
+#define FSG_IOV_TOO_SMALL 4
 
 /* Return codes of the host-side calls. */
 #define FSG_SUCCESS 0
@@ -213,6 +225,45 @@ int fsg_decompress_batch_2s(const uint8_t *d_in, const uint64_t *d_in_off,
                             const uint32_t *d_out_cap, uint32_t *d_out_len,
                             int32_t *d_status, uint32_t flags, void *d_workspace,
                             size_t workspace_bytes, void *stream, void *pass1_stream);
+
+/* Batched UncompressAsMuchAsPossible (snappy.cc:1530-1535) over each
+ * message's stream cut into `frag`-byte source pieces, as Source::Peek hands
+ * them out (0 = one piece, a ByteArraySource; flare's cord_buf blocks carry
+ * 8160 bytes).  d_out slots as for fsg_decompress_batch, sized for the
+ * header's length.  Per message: d_produced[i] = the reference's return value
+ * (SnappyScatteredWriter::Produced(), which counts the 64 KiB block a failing
+ * SlowAppend just filled twice); d_got[i] = the bytes its sink receives, which
+ * are d_out[d_out_off[i] .. + d_got[i]), byte-identical to the reference's.
+ * d_status[i]: FSG_OK (the whole stream decoded), FSG_CORRUPT (it stopped
+ * early), FSG_BAD_HEADER (produced 0), or FSG_SLOT_TOO_SMALL (the reference
+ * would write past the slot; d_got / d_produced 0).  Workspace as for
+ * fsg_decompress_batch.  Streams the batch decoder accepts cost what a
+ * decompress costs; the others are walked serially, one lane each. */
+int fsg_decompress_batch_partial(const uint8_t *d_in, const uint64_t *d_in_off,
+                                 const uint32_t *d_in_len, uint32_t n_msgs, uint32_t frag,
+                                 uint8_t *d_out, const uint64_t *d_out_off,
+                                 const uint32_t *d_out_cap, uint32_t *d_got,
+                                 uint64_t *d_produced, int32_t *d_status, void *d_workspace,
+                                 size_t workspace_bytes, void *stream);
+
+/* Batched RawUncompressToIOVec (snappy.cc:1122-1132).  Message i's iovecs
+ * are entries [d_iov_first[i], d_iov_first[i + 1]) of d_iov_base (device
+ * addresses) / d_iov_len; d_iov_first has n_msgs + 1 entries.  The stream is
+ * decoded into the caller's staging slot (d_stage / d_stage_off / d_stage_cap,
+ * sized for the header's length, as fsg_decompress_batch's output) and then
+ * copied into the iovecs in order, filling each before the next, as
+ * SnappyIOVecWriter does.  d_out_len[i] = the header's length.  d_status[i]:
+ * FSG_OK (the reference's true; the iovecs hold its bytes, bytes past the
+ * length untouched), FSG_CORRUPT / FSG_BAD_HEADER / FSG_IOV_TOO_SMALL (its
+ * false; the iovecs are left untouched, where the reference leaves a decoded
+ * prefix), or FSG_SLOT_TOO_SMALL (staging sizing error). */
+int fsg_decompress_batch_iovec(const uint8_t *d_in, const uint64_t *d_in_off,
+                               const uint32_t *d_in_len, uint32_t n_msgs,
+                               const uint64_t *d_iov_base, const uint64_t *d_iov_len,
+                               const uint32_t *d_iov_first, uint8_t *d_stage,
+                               const uint64_t *d_stage_off, const uint32_t *d_stage_cap,
+                               uint32_t *d_out_len, int32_t *d_status, void *d_workspace,
+                               size_t workspace_bytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -26,6 +26,15 @@ def _buf(b: bytes):
     return ctypes.create_string_buffer(b, max(len(b), 1))
 
 
+def _iovec_call(fn, comp: bytes, iov_lens, fill: int):
+    bufs = [ctypes.create_string_buffer(bytes([fill]) * max(int(n), 1)) for n in iov_lens]
+    cnt = len(bufs)
+    base = (ctypes.c_void_p * max(cnt, 1))(*[ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_size_t * max(cnt, 1))(*[int(n) for n in iov_lens])
+    ok = fn(_buf(comp), len(comp), base, lens, cnt)
+    return bool(ok), [b.raw[:int(n)] for b, n in zip(bufs, iov_lens)]
+
+
 class Oracle:
     def __init__(self, path: Path = ORACLE_LIB):
         if not Path(path).exists():
@@ -43,6 +52,9 @@ class Oracle:
         L.so_compress_batch.restype = _c.c_double
         L.so_uncompress_batch.argtypes = [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _c.c_int]
         L.so_uncompress_batch.restype = _c.c_double
+        L.so_uncompress_as_much.argtypes = [_vp, _sz, _sz, _vp, _sz, _c.POINTER(_sz)]
+        L.so_uncompress_as_much.restype = _sz
+        L.so_uncompress_iovec.argtypes = [_vp, _sz, _vp, _vp, _sz]
         self.L = L
 
     def max_compressed_length(self, n: int) -> int:
@@ -76,6 +88,17 @@ class Oracle:
 
     def is_valid(self, comp: bytes) -> bool:
         return bool(self.L.so_is_valid(_buf(comp), len(comp)))
+
+    def uncompress_as_much(self, comp: bytes, cap: int, frag: int = 0):
+        """UncompressAsMuchAsPossible restated: (its return value, the bytes the sink gets)."""
+        out = ctypes.create_string_buffer(max(cap, 1))
+        got = _sz(0)
+        r = self.L.so_uncompress_as_much(_buf(comp), len(comp), frag, out, cap, ctypes.byref(got))
+        return r, out.raw[:min(got.value, cap)]
+
+    def uncompress_iovec(self, comp: bytes, iov_lens, fill: int = 0xA5):
+        """RawUncompressToIOVec restated: (ok, the iovecs' bytes after the call)."""
+        return _iovec_call(self.L.so_uncompress_iovec, comp, iov_lens, fill)
 
     def compress_batch(self, data, offs, lens, out, out_offs, out_lens, threads=1) -> float:
         return self.L.so_compress_batch(data.ctypes.data, offs.ctypes.data, lens.ctypes.data, len(lens),
@@ -112,6 +135,7 @@ class Reference:
         L.ref_uncompress_as_much.restype = _sz
         L.ref_batch.argtypes = [_c.c_int, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _c.c_int, _sz]
         L.ref_batch.restype = _c.c_double
+        L.ref_uncompress_iovec.argtypes = [_vp, _sz, _vp, _vp, _sz]
         self.L = L
 
     @staticmethod
@@ -136,6 +160,10 @@ class Reference:
         r = self.L.ref_uncompress_as_much(_buf(comp), len(comp), out, cap, frag, ctypes.byref(got))
         assert got.value <= cap
         return r, out.raw[:got.value]
+
+    def uncompress_iovec(self, comp: bytes, iov_lens, fill: int = 0xA5):
+        """RawUncompressToIOVec: (its bool, the iovecs' bytes after the call)."""
+        return _iovec_call(self.L.ref_uncompress_iovec, comp, iov_lens, fill)
 
     def header_source(self, comp: bytes):
         u = _u32(0)

@@ -122,6 +122,17 @@ size_t ref_uncompress_as_much(const char* in, size_t n, char* out, size_t cap, s
   *got = sink.size();
   return r;
 }
+// snappy::RawUncompressToIOVec(const char*, size_t, const iovec*, size_t)
+// (snappy.cc:1122-1132): the reference's bool; the iovecs as it leaves them.
+int ref_uncompress_iovec(const char* in, size_t n, char* const* base, const size_t* len,
+                         size_t cnt) {
+  std::vector<flare::snappy::iovec> iov(cnt ? cnt : 1);
+  for (size_t i = 0; i < cnt; ++i) {
+    iov[i].iov_base = base[i];
+    iov[i].iov_len = len[i];
+  }
+  return flare::snappy::RawUncompressToIOVec(in, n, iov.data(), cnt) ? 1 : 0;
+}
 int ref_is_valid(const char* in, size_t n) {
   return flare::snappy::IsValidCompressedBuffer(in, n) ? 1 : 0;
 }

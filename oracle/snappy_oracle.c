@@ -291,6 +291,230 @@ int so_is_valid(const uint8_t *in, size_t n) {
 }
 
 /* ---------------------------------------------------------------------------
+ * The tag loop once more, with the writer as a parameter: DecompressAllTags
+ * (snappy.cc:716-787) over a source whose Peek hands out `frag`-byte pieces
+ * of the stream (0 = one piece; the ref harness's FragmentSource), RefillTag
+ * (:790-847) stitching a tag across pieces.  A literal is appended piece by
+ * piece (:751-761): the writer sees one Append per piece it spans, and a
+ * literal cut by the end of input appends what the input holds, then stops.
+ * A copy is one AppendFromSelf. */
+typedef struct {
+  int (*append)(void *w, const uint8_t *p, size_t n);
+  int (*append_from_self)(void *w, size_t offset, size_t len);
+  /* TryFastAppend (NULL: the writer's fast path leaves nothing observable) */
+  int (*try_fast)(void *w, const uint8_t *p, size_t available, size_t len);
+} writer_ops_t;
+
+static size_t piece_left(size_t pos, size_t n, size_t frag) {
+  if (pos >= n) return 0;
+  if (!frag) return n - pos;
+  size_t end = (pos / frag + 1) * frag;
+  return (end < n ? end : n) - pos;
+}
+
+/* Returns 1 iff the input ends between tags (the caller checks the length). */
+static int tag_loop(const uint8_t *in, size_t n, size_t pos, size_t frag, void *w,
+                    const writer_ops_t *ops) {
+  for (;;) {
+    if (pos == n) return 1;
+    uint32_t c = in[pos];
+    uint32_t extra = (c & 3) == 0 ? ((c >> 2) + 1 > 60 ? (c >> 2) + 1 - 60 : 0)
+                                   : ((c & 3) == 1 ? 1 : ((c & 3) == 2 ? 2 : 4));
+    if (n - pos < 1 + (size_t)extra) return 0; /* RefillTag: a cut tag */
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < extra; ++k) v |= (uint32_t)in[pos + 1 + k] << (8 * k);
+    pos += 1 + extra;
+    if ((c & 3) == 0) {
+      size_t len = extra ? (size_t)(uint32_t)(v + 1u) : (size_t)((c >> 2) + 1);
+      /* :736: tried right after the tag byte, before any length bytes */
+      if (!extra && ops->try_fast && ops->try_fast(w, in + pos, piece_left(pos, n, frag), len)) {
+        pos += len;
+        continue;
+      }
+      for (;;) {
+        size_t a = piece_left(pos, n, frag);
+        if (a >= len) {
+          if (len && !ops->append(w, in + pos, len)) return 0;
+          pos += len;
+          break;
+        }
+        if (a == 0) return 0; /* premature end of input */
+        if (!ops->append(w, in + pos, a)) return 0;
+        pos += a;
+        len -= a;
+      }
+    } else {
+      uint32_t len = (c & 3) == 1 ? 4 + ((c >> 2) & 7) : (c >> 2) + 1;
+      uint32_t offset = (c & 3) == 1 ? (((c >> 5) << 8) | v) : v;
+      if (!ops->append_from_self(w, offset, len)) return 0;
+    }
+  }
+}
+
+/* SnappyScatteredWriter (snappy.cc:1331-1481): output in blocks of
+ * kBlockSize (the last one cut at the header's length), SlowAppend filling
+ * the current block before its bounds check (:1424-1451).  Bytes land at
+ * their output positions in `out`; the ones past `cap` are counted, not
+ * stored (the harness's copying sink). */
+typedef struct {
+  uint8_t *out;
+  size_t cap, expected, full, blk_len, blk_used, hi;
+} scatter_t;
+
+static void sc_put(scatter_t *s, const uint8_t *p, size_t n) {
+  size_t at = s->full + s->blk_used;
+  for (size_t i = 0; i < n; ++i)
+    if (at + i < s->cap) s->out[at + i] = p[i];
+  s->blk_used += n;
+  if (at + n > s->hi) s->hi = at + n;
+}
+
+static int sc_append(void *w, const uint8_t *p, size_t len) {
+  scatter_t *s = (scatter_t *)w;
+  size_t avail = s->blk_len - s->blk_used;
+  while (len > avail) {
+    sc_put(s, p, avail);
+    s->full += s->blk_used; /* full_size_ += op_ptr_ - op_base_ */
+    len -= avail;
+    p += avail;
+    if (s->full + len > s->expected) return 0; /* op_base_ / op_ptr_ keep the filled block */
+    s->blk_len = s->expected - s->full < BLOCK_SIZE ? s->expected - s->full : BLOCK_SIZE;
+    s->blk_used = 0;
+    avail = s->blk_len;
+  }
+  sc_put(s, p, len);
+  return 1;
+}
+
+static int sc_append_from_self(void *w, size_t offset, size_t len) {
+  scatter_t *s = (scatter_t *)w;
+  size_t cur = s->full + s->blk_used;
+  if (offset - 1u >= cur || s->expected - cur < len) return 0; /* :1463-1466 */
+  for (size_t i = 0; i < len; ++i) {
+    size_t src = cur - offset + i;
+    uint8_t c = src < s->cap ? s->out[src] : 0;
+    sc_append(s, &c, 1);
+  }
+  return 1;
+}
+
+size_t so_uncompress_as_much(const uint8_t *in, size_t n, size_t frag, uint8_t *out,
+                             size_t cap, size_t *got) {
+  static const writer_ops_t ops = {sc_append, sc_append_from_self, NULL};
+  uint32_t ulen = 0;
+  *got = 0;
+  int h = so_header_lenient(in, n, &ulen); /* InternalUncompress :858-868 */
+  if (!h) return 0;
+  scatter_t s = {out, cap, ulen, 0, 0, 0, 0};
+  (void)tag_loop(in, n, (size_t)h, frag, &s, &ops);
+  *got = s.hi;                   /* Flush(Produced()): every byte written */
+  return s.full + s.blk_used;    /* Produced() */
+}
+
+/* SnappyIOVecWriter (snappy.cc:963-1120): the output limit is the header's
+ * length; iovecs fill in order, a full one moves on to the next, and running
+ * out of iovecs fails the call.  AppendFromSelf locates its source by
+ * walking back over earlier (full) iovecs and copies through Append, whose
+ * result it does not check (:1078-1086), or byte by byte inside the current
+ * iovec (IncrementalCopy, :1106-1108). */
+typedef struct {
+  uint8_t *const *base;
+  const size_t *len;
+  size_t cnt, cur, written, total, limit;
+} iovw_t;
+
+static int iov_append(void *w, const uint8_t *p, size_t len) {
+  iovw_t *s = (iovw_t *)w;
+  if (s->total + len > s->limit) return 0;
+  while (len > 0) {
+    if (s->written >= s->len[s->cur]) {
+      if (s->cur + 1 >= s->cnt) return 0;
+      s->written = 0;
+      ++s->cur;
+    }
+    size_t k = s->len[s->cur] - s->written;
+    if (k > len) k = len;
+    memmove(s->base[s->cur] + s->written, p, k);
+    s->written += k;
+    s->total += k;
+    p += k;
+    len -= k;
+  }
+  return 1;
+}
+
+static int iov_append_from_self(void *w, size_t offset, size_t len) {
+  iovw_t *s = (iovw_t *)w;
+  if (offset > s->total || offset == 0) return 0;
+  if (len > s->limit - s->total) return 0;
+  size_t fi = s->cur, fo = s->written;
+  while (offset > 0) {
+    if (fo >= offset) {
+      fo -= offset;
+      break;
+    }
+    offset -= fo;
+    --fi;
+    fo = s->len[fi];
+  }
+  while (len > 0) {
+    if (fi != s->cur) {
+      size_t k = s->len[fi] - fo;
+      if (k > len) k = len;
+      (void)iov_append(s, s->base[fi] + fo, k);
+      len -= k;
+      if (len > 0) {
+        ++fi;
+        fo = 0;
+      }
+    } else {
+      size_t k = s->len[s->cur] - s->written;
+      if (k == 0) {
+        if (s->cur + 1 >= s->cnt) return 0;
+        ++s->cur;
+        s->written = 0;
+        continue;
+      }
+      if (k > len) k = len;
+      for (size_t i = 0; i < k; ++i) s->base[s->cur][s->written + i] = s->base[fi][fo + i];
+      s->written += k;
+      fo += k;
+      s->total += k;
+      len -= k;
+    }
+  }
+  return 1;
+}
+
+/* :1035-1049: 16 bytes copied when the input, the output limit and the
+ * current iovec all have 16 bytes of room; only `len` of them count (the
+ * rest is overwritten later, or left behind when the call fails) */
+static int iov_try_fast(void *w, const uint8_t *p, size_t available, size_t len) {
+  iovw_t *s = (iovw_t *)w;
+  if (len <= 16 && available >= 16 + 5 && s->limit - s->total >= 16 &&
+      s->len[s->cur] - s->written >= 16) {
+    memmove(s->base[s->cur] + s->written, p, 16);
+    s->written += len;
+    s->total += len;
+    return 1;
+  }
+  return 0;
+}
+
+int so_uncompress_iovec(const uint8_t *in, size_t n, uint8_t *const *iov_base,
+                        const size_t *iov_len, size_t iov_cnt) {
+  static const writer_ops_t ops = {iov_append, iov_append_from_self, iov_try_fast};
+  uint32_t ulen = 0;
+  int h = so_header_lenient(in, n, &ulen); /* RawUncompressToIOVec :1122-1132 */
+  if (!h) return 0;
+  /* no iovecs and output to place: the reference reads iov[0] (undefined);
+   * with ulen 0 no Append ever reaches the iovecs */
+  if (iov_cnt == 0 && ulen > 0) return 0;
+  iovw_t s = {iov_base, iov_len, iov_cnt, 0, 0, 0, ulen};
+  return tag_loop(in, n, (size_t)h, 0, &s, &ops) && s.total == ulen;
+}
+
+/* ---------------------------------------------------------------------------
  * Batched CPU baseline: threads own strided message indices. */
 typedef struct {
   int tid, nthreads, mode;

@@ -16,7 +16,8 @@ GOLDEN = Path(__file__).resolve().parent / "golden"
 def test_header_declares_expected_entry_points():
     syms = fsg.header_symbols()
     for s in ("fsg_compress_batch", "fsg_decompress_batch", "fsg_max_compressed_length",
-              "fsg_get_uncompressed_length", "fsg_init"):
+              "fsg_get_uncompressed_length", "fsg_init", "fsg_decompress_batch_partial",
+              "fsg_decompress_batch_iovec"):
         assert s in syms
 
 
@@ -54,6 +55,11 @@ def test_invalid_arguments_rejected_without_gpu():
     rc = lib.fsg_compress_batch(None, None, None, 5, 0, None, None, None, None, None, 0, None)
     assert rc == -1
     rc = lib.fsg_decompress_batch(None, None, None, 5, None, None, None, None, None, 0, None, 0, None)
+    assert rc == -1
+    rc = lib.fsg_decompress_batch_partial(None, None, None, 5, 0, None, None, None, None, None, None, None, 0, None)
+    assert rc == -1
+    rc = lib.fsg_decompress_batch_iovec(None, None, None, 5, None, None, None, None, None, None, None, None, None,
+                                        0, None)
     assert rc == -1
 
 

@@ -183,3 +183,81 @@ def test_full_size_fixtures(oracle, name):
         assert len(c) == f["compressed_len"][i], i
         if name != "CM":
             assert fsg.fnv1a64(c) == f["compressed_fnv"][i] and fsg.fnv1a64(x) == f["input_fnv"][i], i
+
+
+# ---- UncompressAsMuchAsPossible and RawUncompressToIOVec restated
+# (snappy.cc:1530-1535, :963-1132): pinned to the negative.json fixtures
+# (made by the reference, 8160-byte source pieces) and to the reference build.
+
+@pytest.mark.parametrize("v", _negatives(), ids=lambda v: v["name"])
+def test_oracle_as_much_golden(oracle, v):
+    if v["ok"] is None or not v["header_ok"]:
+        return
+    r, got = oracle.uncompress_as_much(bytes.fromhex(v["hex"]), v["ulen"], frag=8160)
+    assert r == v["partial_ret"]
+    assert len(got) == v["partial_len"]
+    assert "%016x" % fsg.fnv1a64(got) == v["partial_fnv"]
+
+
+def _mutants(oracle, rng, count):
+    srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (40, 900, 20000, 70000, 140000)]
+    for _ in range(count):
+        c = bytearray(oracle.compress(rng.choice(srcs)))
+        for _ in range(rng.randint(0, 3)):
+            c[rng.randrange(len(c))] = rng.randrange(256)
+        if rng.random() < 0.3:
+            c = c[: rng.randrange(1, len(c) + 1)]
+        yield bytes(c)
+
+
+@pytest.mark.skipif(not Reference.available(), reason="oracle/_ref not built here")
+def test_oracle_as_much_matches_reference(oracle):
+    ref = Reference()
+    rng = random.Random(23)
+    n_partial = 0
+    for c in _mutants(oracle, rng, 600):
+        h, ulen = oracle.header(c)
+        if not h or ulen > 1 << 20:
+            continue
+        frag = rng.choice([0, 1, 7, 8160])
+        r, got = oracle.uncompress_as_much(c, ulen, frag)
+        rr, rgot = ref.uncompress_as_much(c, ulen, frag if frag else len(c))
+        assert (r, got) == (rr, rgot), frag
+        n_partial += r != ulen
+    assert n_partial > 50
+
+
+def _iov_split(rng, total):
+    """Random iovec lengths: empty ones, exact, short and roomy lists."""
+    k = rng.randint(1, 6)
+    cuts = sorted(rng.randint(0, total) for _ in range(k - 1))
+    lens = [b - a for a, b in zip([0] + cuts, cuts + [total])]
+    mode = rng.random()
+    if mode < 0.2 and lens:
+        lens[-1] += rng.randint(1, 40)          # room to spare
+    elif mode < 0.35 and total:
+        lens[rng.randrange(len(lens))] = max(0, lens[-1] - rng.randint(1, 20))  # too short
+    if rng.random() < 0.3:
+        lens.insert(rng.randrange(len(lens) + 1), 0)
+    return lens
+
+
+@pytest.mark.skipif(not Reference.available(), reason="oracle/_ref not built here")
+def test_oracle_iovec_matches_reference(oracle):
+    ref = Reference()
+    rng = random.Random(29)
+    seen = {True: 0, False: 0}
+    for c in _mutants(oracle, rng, 600):
+        h, ulen = oracle.header(c)
+        if not h or ulen > 1 << 20:
+            continue
+        lens = _iov_split(rng, ulen)
+        ok, bufs = oracle.uncompress_iovec(c, lens)
+        rok, rbufs = ref.uncompress_iovec(c, lens)
+        assert ok == rok
+        assert bufs == rbufs  # the prefix the reference leaves on failure too
+        if ok:
+            flat = oracle.uncompress(c)[2]
+            assert b"".join(bufs)[:ulen] == flat
+        seen[ok] += 1
+    assert seen[True] > 50 and seen[False] > 50
