@@ -684,7 +684,14 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
     u32 per_cu = (160u * 1024u) / (lds + (u32)encode_wave_static_lds_bytes());
     const i64 pc_opt = opt(kOptEncodeWavePerCu);
     if (pc_opt > 0 && (u64)pc_opt < per_cu) per_cu = (u32)pc_opt;
-    const u32 waves = 256u * (per_cu ? per_cu : 1u);
+    u32 waves = 256u * (per_cu ? per_cu : 1u);
+    // A small batch has at most n_msgs x fragments units; the waves past
+    // them find no unit but are still dispatched (one 4 KiB body: 5,120
+    // waves of 8 KiB tables, in front of the lanes' launch).
+    if (n_msgs <= kSmallBatchEnc) {
+      const u64 units = (u64)n_msgs * (((u64)max_in_len + kBlockSize - 1) >> kBlockLog);
+      if (units && units < waves) waves = (u32)units;
+    }
     hipStream_t wstream = stream;
     if (side) {
       lk = std::unique_lock<std::mutex>(side->mu);
