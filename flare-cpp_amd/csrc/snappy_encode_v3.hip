@@ -685,10 +685,10 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
     const i64 pc_opt = opt(kOptEncodeWavePerCu);
     if (pc_opt > 0 && (u64)pc_opt < per_cu) per_cu = (u32)pc_opt;
     u32 waves = 256u * (per_cu ? per_cu : 1u);
-    // A small batch has at most n_msgs x fragments units; the waves past
-    // them find no unit but are still dispatched (one 4 KiB body: 5,120
-    // waves of 8 KiB tables, in front of the lanes' launch).
-    if (n_msgs <= kSmallBatchEnc) {
+    // A batch has at most n_msgs x fragments units; the waves past them find
+    // no unit but are still dispatched (one 4 KiB body: 5,120 waves of 8 KiB
+    // tables, ~60 us in front of the lanes' launch).
+    {
       const u64 units = (u64)n_msgs * (((u64)max_in_len + kBlockSize - 1) >> kBlockLog);
       if (units && units < waves) waves = (u32)units;
     }
