@@ -24,7 +24,9 @@ import fsg  # noqa: E402
 
 WL = {"c3": (fsg.KIND_TEXT, 65536, 65536), "c5": (fsg.KIND_PROTO, 262144, None),
       "c3w": (fsg.KIND_TEXT, 65536, 65536), "c5w": (fsg.KIND_PROTO, 262144, None),
-      "c3s": (fsg.KIND_TEXT, 8192, 65536)}
+      "c3s": (fsg.KIND_TEXT, 8192, 65536),
+      "s4k": (fsg.KIND_TEXT, 131072, 4096), "s8k": (fsg.KIND_TEXT, 65536, 8192),
+      "s2k": (fsg.KIND_TEXT, 131072, 2048)}
 
 
 def main():
