@@ -30,6 +30,7 @@ hipError_t launch_headers(const u8* in, const u64* in_off, const u32* in_len,
                           u32 n_msgs, u32* ulen, int lenient, hipStream_t stream);
 size_t encode_tables_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out);
 size_t encode_plan_bytes(u32 n_msgs, u32 max_in_len);
+bool encode_all_on_wave(u32 n_msgs, u32 max_in_len);
 hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                             u32* out_len, i32* status, void* ws, size_t ws_bytes,
@@ -267,7 +268,7 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
     const fsg::u32 wmin = encode_wave_min();
     if (lanes_cap) {
       if (lanes_cap < slots) slots = (lanes_cap + 63) / 64 * 64;
-    } else if (wmin && max_in_len >= wmin && n_msgs > 64) {
+    } else if (wmin && n_msgs > 64 && (max_in_len >= wmin || fsg::encode_all_on_wave(n_msgs, max_in_len))) {
       fsg::u32 beside = (fsg::u32)(((uint64_t)n_msgs * 3 / 4 + 255) / 256 * 256);
       if (beside > 131072u) beside = 131072u;
       if (beside < slots) slots = beside;

@@ -592,8 +592,21 @@ size_t encode_tables_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out)
 // message encoded whole by one lane.)
 constexpr u32 kWaveMinBound = 4096;  // smallest wave_min the plan region is sized for
 constexpr u32 kSmallBatchEnc = 64;   // batches of at most this many messages: every message on the wave encoder
+// Batches of short bodies only (at most this many bytes each): every message
+// on the wave encoder too.  Their tables are small (8 KiB for 4 KiB bodies),
+// so many waves fit per CU, and nothing else in the batch needs the LDS:
+// 131,072 x 4 KiB text 19.1 -> 8.6 ms, 65,536 x 8 KiB 18.5 -> 11.4 ms
+// against the lanes.
+#ifndef FSG_ENC_ALL_WAVE_MAX
+#define FSG_ENC_ALL_WAVE_MAX 8192
+#endif
+constexpr u32 kAllWaveMax = FSG_ENC_ALL_WAVE_MAX;
+__host__ __device__ inline bool all_on_wave(u32 n_msgs, u32 max_in_len) {
+  return max_in_len >= kInputMarginBytes && (n_msgs <= kSmallBatchEnc || max_in_len <= kAllWaveMax);
+}
+bool encode_all_on_wave(u32 n_msgs, u32 max_in_len) { return all_on_wave(n_msgs, max_in_len); }
 size_t encode_plan_bytes(u32 n_msgs, u32 max_in_len) {
-  if (max_in_len < kWaveMinBound && !(n_msgs <= kSmallBatchEnc && max_in_len >= kInputMarginBytes)) return 0;
+  if (max_in_len < kWaveMinBound && !all_on_wave(n_msgs, max_in_len)) return 0;
   u64 per_msg = ((u64)max_in_len + kBlockSize - 1) >> kBlockLog;
   if (per_msg < 1) per_msg = 1;
   const u64 max_items = (u64)n_msgs * per_msg;
@@ -647,10 +660,10 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
   const bool can_split = max_in_len > kBlockSize;
   if (wave_min && wave_min < kWaveMinBound) wave_min = kWaveMinBound;
   // A batch of at most one wave of messages (the host runtime's one-caller
-  // batches): every message on the wave encoder, whose latency for one
-  // message is a fraction of one lane's (4 KiB text: ~0.3 ms against 1.1 ms
-  // measured in the C1 echo trace)
-  if (wave_min && n_msgs <= kSmallBatchEnc) wave_min = kInputMarginBytes;
+  // batches: the wave encoder's latency for one message is a fraction of one
+  // lane's, 4 KiB text ~0.2 ms against 1.1 ms in the C1 echo trace), or of
+  // short bodies only (kAllWaveMax): every message on the wave encoder
+  if (wave_min && all_on_wave(n_msgs, max_in_len)) wave_min = kInputMarginBytes;
   if (max_in_len < wave_min) wave_min = 0;  // nothing long enough (or no bound known)
   if (plan && ws_bytes >= tables_bytes + plan && (can_split || wave_min)) {
     const u64 max_items = (plan - 256 - (u64)n_msgs * 8) / 12;

@@ -26,7 +26,7 @@ WL = {"c3": (fsg.KIND_TEXT, 65536, 65536), "c5": (fsg.KIND_PROTO, 262144, None),
       "c3w": (fsg.KIND_TEXT, 65536, 65536), "c5w": (fsg.KIND_PROTO, 262144, None),
       "c3s": (fsg.KIND_TEXT, 8192, 65536),
       "s4k": (fsg.KIND_TEXT, 131072, 4096), "s8k": (fsg.KIND_TEXT, 65536, 8192),
-      "s2k": (fsg.KIND_TEXT, 131072, 2048)}
+      "s2k": (fsg.KIND_TEXT, 131072, 2048), "c2r": (fsg.KIND_RANDOM, 65536, 4096)}
 
 
 def main():
