@@ -95,8 +95,11 @@ def test_as_much_golden(codec):
     assert quirk > 0
 
 
-@pytest.mark.parametrize("frag", [0, 7, 8160])
-def test_as_much_fuzz_against_oracle(codec, oracle, frag):
+@pytest.mark.parametrize("frag,fork", [(0, 0), (7, 0), (8160, 0), (8160, 1)])
+def test_as_much_fuzz_against_oracle(codec, oracle, frag, fork, fsg_opts):
+    """fork 1: the batch decoder under it takes the path of batches over 128K
+    messages (plan pass, side streams), forced on this batch."""
+    fsg_opts(decode_fork=fork)
     rng = np.random.default_rng(31 + frag)
     comps = _mutants(oracle, rng, 1500)
     comps += [oracle.compress(fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0)) for s in (0, 1, 20, 65536)]
@@ -177,8 +180,10 @@ def _iovec(codec, comps, iov_lens):
     return st, bufs, guards, caps, ulens
 
 
-def test_iovec_fuzz_against_oracle(codec, oracle):
-    rng = np.random.default_rng(41)
+@pytest.mark.parametrize("fork", [0, 1])
+def test_iovec_fuzz_against_oracle(codec, oracle, fork, fsg_opts):
+    fsg_opts(decode_fork=fork)
+    rng = np.random.default_rng(41 + fork)
     comps = _mutants(oracle, rng, 1200)
     comps += [oracle.compress(fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0)) for s in (0, 1, 20, 65536)]
     hdr = [oracle.header(c) for c in comps]
