@@ -5,7 +5,7 @@ ARCH     ?= gfx950
 PKG      := flare-cpp_amd
 LIB      := $(PKG)/lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall
-CSRC     := $(PKG)/csrc/capi.hip $(PKG)/csrc/snappy_decode.hip $(PKG)/csrc/snappy_decode_v3.hip $(PKG)/csrc/snappy_decode_v4.hip $(PKG)/csrc/snappy_decode_tiny.hip $(PKG)/csrc/snappy_decode_partial.hip \
+CSRC     := $(PKG)/csrc/capi.hip $(PKG)/csrc/snappy_decode.hip $(PKG)/csrc/snappy_decode_v3.hip $(PKG)/csrc/snappy_decode_v4.hip $(PKG)/csrc/snappy_decode_partial.hip \
             $(PKG)/csrc/snappy_encode.hip $(PKG)/csrc/snappy_encode_v3.hip $(PKG)/csrc/snappy_encode_wave.hip $(PKG)/csrc/gather.hip $(PKG)/csrc/lz4.hip $(PKG)/csrc/lz4_decode2.hip
 CHDRS    := $(PKG)/csrc/options.h $(PKG)/csrc/snappy_device.h $(PKG)/csrc/snappy_lane_decode.h $(PKG)/csrc/snappy_pieces.h $(PKG)/csrc/wave_util.h include/flare_snappy_gpu.h include/flare_lz4_gpu.h
 OBJDIR   := build/obj

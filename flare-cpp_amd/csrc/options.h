@@ -26,8 +26,6 @@ enum Opt : int {
   kOptExecBigBlocks,      // one-stream exec launch: large-message blocks
   kOptExecPrio,           // exec pass priority raise around round-A loads
   kOptExecBigBlocksFork,  // forked path: large-message exec blocks
-  kOptDiagNoTail,         // diagnostic: skip the trailing fallback launch
-  kOptTinyPass,           // forked path: bodies < 512 B compressed one per lane (snappy_decode_tiny.hip; off: slower)
   // Snappy encode (capi.hip, snappy_encode_v3.hip)
   kOptEncodeWaveMin,      // long-unit threshold of the wave encoder (bytes; 0 = lanes only)
   kOptEncodeWaveShare,    // wave encoder's share of long units (permille)

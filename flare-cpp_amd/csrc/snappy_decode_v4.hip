@@ -46,10 +46,6 @@
 
 namespace fsg {
 
-hipError_t launch_tiny(const u8* in, const u64* in_off, const u32* in_len, u8* out, const u64* out_off,
-                       const u32* out_len, i32* status, const u32* walk_perm, const u32* walk_hist,
-                       u32 walk_classes, u32 tiny_class, u32 blocks, hipStream_t stream);
-
 namespace {
 
 // ---- pass 1 geometry (per-lane LDS ring of input chunks, as v3)
@@ -58,31 +54,13 @@ namespace {
 constexpr int kIdxTagsOne = 32, kIdxTagsPlanned = 24;
 // Input bounds of the lane walk checked once per iteration instead of per
 // tag (see the walk): ~5 fewer VALU per tag step.
-#ifndef FSG_IDX_ITER_CHECK
-#define FSG_IDX_ITER_CHECK 1
-#endif
 // Pass 1b walks two 64-byte windows per step (see index_big_message).
-#ifndef FSG_BIG_TWO_WINDOWS
-#define FSG_BIG_TWO_WINDOWS 1
-#endif
 // Pass 1b's priority on the forked path's non-huge set (A/B knob; 0 = none).
-#ifndef FSG_BIG_PRIO
-#define FSG_BIG_PRIO 0
-#endif
 // The one-stream lane walk stores its bitmap four groups at a time (see
 // index_kernel).
-#ifndef FSG_IDX_SUPER
-#define FSG_IDX_SUPER 1
-#endif
 // The tag-start bitmap is written whole by the index passes instead of
 // zeroed by the launch (see the lane walk's group stores).
-#ifndef FSG_BITMAP_NOZERO
-#define FSG_BITMAP_NOZERO 1
-#endif
 // Rounds B with pattern chunks outside the common path (see exec5_message).
-#ifndef FSG_ROUNDS_V2
-#define FSG_ROUNDS_V2 1
-#endif
 constexpr u32 kRingChunks = 16;              // 16-byte chunks per lane (256 B)
 constexpr u32 kAhead = 7;                    // chunks prefetched per iteration
 // Waves per pass-1 workgroup.  One: most resident waves for large batches
@@ -254,11 +232,6 @@ __device__ __forceinline__ i32 index_prologue(
 
 // Size classes of the planned lane walk (see index_plan_kernel).
 constexpr u32 kWalkClasses = 16;
-// The tiny-body pass (snappy_decode_tiny.hip): walk classes >= kTinyClass,
-// i.e. compressed size < 2^(15 - kTinyClass + 1) = 512 B; two one-wave blocks
-// per CU (its LDS: 68.9 KB per block).
-constexpr u32 kTinyClass = 7;
-constexpr u32 kTinyBlocks = 512;
 __device__ __forceinline__ u32 walk_class(u32 n_in) {
   const u32 lg = 31u - (u32)__builtin_clz(n_in | 1u);
   return kWalkClasses - 1 - (lg < kWalkClasses - 1 ? lg : kWalkClasses - 1);
@@ -364,8 +337,8 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   // left the XCD's L2 between stores and every 16-byte store cost a line
   // write (0.90 GB written for C3's 0.27 GB bitmap).  Its ring
   // then holds 8 groups: the groups since the last stored super-group (<= 3)
-  // plus the <= 3 an iteration spans.  FSG_IDX_SUPER=0: one group at a time.
-  constexpr bool kSuper = FSG_IDX_SUPER && !kPlanned && !kLean;
+  // plus the <= 3 an iteration spans.
+  constexpr bool kSuper = !kPlanned && !kLean;
   constexpr u32 kBG = kLean ? 2 : (kSuper ? 8 : 4), kBW = 4 * kBG;
   // per wave, [dword][lane]; dword 64 = copy of dword 0; 65..68 absorb
   // unused prefetches
@@ -415,8 +388,8 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   // first one of class split_class -- the larger / the smaller bodies)
   const bool ordered = kPlanned && walk_perm;
   const u32 n_walk = ordered ? walk_hist[2 * kWalkClasses] : n_msgs;
-  // (split_class bits 8-15, when set: the first class the tiny-body pass
-  // takes -- positions from its first one are not walked here)
+  // (split_class bits 8-15, when set: the first class another pass takes --
+  // positions from its first one are not walked here; no pass sets it now)
   const u32 tcls = split_class >> 8;
   const u32 split = walk_part ? walk_hist[kWalkClasses + (split_class & 0xffu)] : 0u;
   const u32 t_hi = tcls ? walk_hist[kWalkClasses + tcls] : n_walk;
@@ -524,9 +497,7 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     u32 lo, hi;
     ring_read(ip, lo, hi);
     const u32 op_it = op;
-#if FSG_IDX_ITER_CHECK
     u32 lmax = 0;  // the largest long-literal length looked at this iteration
-#endif
 #pragma unroll
     for (int j = 0; j < kIdxTags; ++j) {
       const u32 bsh = (ip + ibal) & 3;
@@ -554,7 +525,6 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
       const u32 step = adv + lpart;
       const u32 ip_next = look ? ip + step : ip;
       if (j + 1 < kIdxTags) ring_read(ip_next, lo, hi);
-#if FSG_IDX_ITER_CHECK
       // Bounds are checked once per iteration (below), not per tag: a tag
       // whose bytes run past the input leaves ip_next > n_in (no u32 wrap
       // while lpart <= n_in, since ip <= n_in < 2^31 and adv <= 65), after
@@ -564,28 +534,10 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
       // message never stores.
       lmax = look && lpart > lmax ? lpart : lmax;
       atomicOr(&bmr[((ip >> 5) & (kBW - 1)) * kWave + lane], look ? 1u << (ip & 31) : 0u);
-#else
-      // Tag bytes and literal bytes present (:744-761): the step fits the
-      // bytes left (ip < n_in whenever `look`).  A 4-byte literal length can
-      // wrap the u32 step (the true step is >= 2^32 > any input), which shows
-      // as step < adv.  Copy offsets (:1200, :1410, :1466) are checked by the
-      // exec pass, which has every tag's output position at hand (this pass
-      // only feeds it); the writer's space check (:1166, :1400) is per
-      // iteration, below: op only grows.
-      const bool bad = (step > n_in - ip) | (step < adv);
-      status = (look && bad) ? kCorrupt : status;
-      const bool take = look && !bad;
-      // unconditional (bits land in the LDS ring even without a bitmap): a
-      // per-tag branch here would split the unrolled walk into one basic
-      // block per tag
-      atomicOr(&bmr[((ip >> 5) & (kBW - 1)) * kWave + lane], take ? 1u << (ip & 31) : 0u);
-#endif
       op += look ? len : 0u;
       ip = ip_next;
     }
-#if FSG_IDX_ITER_CHECK
     if (status < 0 && (ip > n_in || lmax > n_in)) status = kCorrupt;
-#endif
     // writer space (:1166, :1400), checked once per iteration: op only grows,
     // and one iteration cannot wrap it (accepted literals fit the input)
     if (status < 0 && (op > expected || op < op_it)) status = kCorrupt;
@@ -593,7 +545,6 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     if (status < 0 && ip == n_in) status = op == expected ? kOk : kCorrupt;
 
     // ---------- store the bit groups the walk has left
-#if FSG_BITMAP_NOZERO
     // The bitmap is not zeroed by the launch: every group of a message the
     // execution pass will read is stored here, zero groups included (a
     // single-literal message's bitmap is never read), and the groups a long
@@ -646,27 +597,6 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
         fg = cur > fg ? cur : fg;
       }
     }
-#else
-    if (bm) {
-      const u32 cur = status < 0 ? ip >> 7 : 0xffffffffu;
-#pragma unroll
-      for (u32 k = 0; k < kBG; ++k) {
-        const u32 gi = fg + k;
-        if (gi < cur) {
-          const u32 sl = (gi & (kBG - 1)) * 4;
-          u32x4 v;
-#pragma unroll
-          for (u32 q = 0; q < 4; ++q) v[q] = bmr[(sl + q) * kWave + lane];
-          if ((v[0] | v[1] | v[2] | v[3]) && status != kCorrupt) {
-            *reinterpret_cast<u32x4*>(bm + 4 * gi) = v;
-#pragma unroll
-            for (u32 q = 0; q < 4; ++q) bmr[(sl + q) * kWave + lane] = 0;
-          }
-        }
-      }
-      fg = cur > fg + kBG ? cur : (cur > fg ? cur : fg);
-    }
-#endif
 
     // ---------- land the chunks loaded last iteration
 #pragma unroll
@@ -727,19 +657,16 @@ __device__ __forceinline__ i32 index_big_message(
   u32 op = 0;
   i32 status = -1;
   u32* bm = bitmap + bm_base[m];
-#if FSG_BITMAP_NOZERO
   {  // the launch does not zero the bitmap: this message's words first
     const u32 words = (((n_in + 31) >> 5) + 3) & ~3u;
     for (u32 wd = 4 * lane; wd < words; wd += 256) *reinterpret_cast<u32x4*>(bm + wd) = u32x4{0, 0, 0, 0};
   }
-#endif
   const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
   const u8* abase = ib - ibal;
   const u32 last_chunk = (ibal + n_in - 1) >> 4;
   int spos = -1;  // message position of stage byte 0 (-1: nothing staged)
   u32 send = 0;   // positions [spos, send) are valid in the stage
 
-#if FSG_BIG_TWO_WINDOWS
   // Two 64-byte windows per step, A = [wb, wb + 64) and B = [wb + 64,
   // wb + 128), each lane decoding one candidate tag in each: the pointer
   // doubling does not depend on where the chain enters a window, so both
@@ -871,104 +798,6 @@ __device__ __forceinline__ i32 index_big_message(
     const u32 wbits = (lane & 1) == 0 ? (u32)Sw : (u32)(Sw >> 32);
     if (lane < 4 && wbits) bm[(wb >> 5) + lane] = wbits;
   }
-#else
-  while (status < 0) {
-    if (ip >= n_in) {  // end of input between tags (snappy.cc:858-868)
-      status = (ip == n_in && op == expected) ? kOk : kCorrupt;
-      break;
-    }
-    const u32 wb = ip & ~31u;
-    // ---------- stage input covering [wb, wb + 64 + 4)
-    if (spos < 0 || wb < (u32)spos || wb + 72 > send) {
-      const u32 c0 = (wb + ibal) >> 4;
-      u32x4 x[kBigStageChunks / 64];
-#pragma unroll
-      for (u32 r = 0; r < kBigStageChunks / 64; ++r) {
-        u32 k = c0 + r * 64 + lane;
-        k = k <= last_chunk ? k : last_chunk;
-        x[r] = *reinterpret_cast<const u32x4*>(abase + 16 * k);
-      }
-      wave_lds_fence();  // previous window's stage reads are done
-#pragma unroll
-      for (u32 r = 0; r < kBigStageChunks / 64; ++r)
-        *reinterpret_cast<u32x4*>(st + 4 * (r * 64 + lane)) = x[r];
-      wave_lds_fence();
-      spos = (int)(16 * c0) - (int)ibal;
-      send = (u32)spos + kBigStageBytes - 8;
-    }
-    // ---------- every lane decodes the tag that would start at wb + lane
-    const u32 p = wb + lane;
-    const u32 s = p - (u32)spos;
-    const u32 dw = s >> 2, bsh = s & 3;
-    const u32 lo = st[dw], hi = st[dw + 1];
-    const u32 t0 = alignbyte(hi, lo, bsh);
-    const u32 b4 = (hi >> (8 * bsh)) & 0xffu;
-    const u32 c = t0 & 0xffu;
-    const u32 type = c & 3;
-    const bool is_lit = type == 0;
-    const u32 l0 = (c >> 2) + 1;
-    const bool longlit = is_lit & (l0 >= 61);
-    const u32 nb = is_lit ? (longlit ? l0 - 60 : 0u) : (1u << (type - 1));
-    const u32 ext = (b4 << 24) | (t0 >> 8);
-    const u32 val = nb >= 4 ? ext : ext & ((1u << (8 * nb)) - 1u);
-    const u32 len = is_lit ? (longlit ? val + 1u : l0) : (type == 1 ? 4 + ((c >> 2) & 7) : l0);
-    const u32 coff = type == 1 ? (((c >> 5) << 8) | val) : val;
-    const u32 avail = n_in - p - 1;
-    // the checks that need no walk state: tag bytes and literal bytes present
-    const bool bad_local = (p >= n_in) | (avail < nb) | (is_lit & (avail - nb < len));
-    const u32 adv = 1 + nb + (is_lit ? len : 0u);
-    const u32 nxt = p + adv;  // next tag position (meaningful when !bad_local)
-
-    // ---------- which lanes are real tag starts: the chain from ip, by
-    // pointer doubling.  J = successor lane (64 = left the window, or reached
-    // the end of input); after round k, M = the lanes visited within 2^k
-    // steps from this lane.  A 64-byte window holds <= 32 tags (>= 2 bytes
-    // each), so 5 rounds cover any chain.
-    u32 J = (bad_local || adv >= 64 - lane || nxt >= n_in) ? 64u : lane + adv;
-    const u32 first = ip - wb;
-    u64 M = 1ull << lane;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const u32 src = J < 64 ? J : lane;
-      const u64 Mj = ((u64)(u32)__shfl((int)(u32)(M >> 32), (int)src, 64) << 32) |
-                     (u32)__shfl((int)(u32)M, (int)src, 64);
-      const u32 Jj = (u32)__shfl((int)J, (int)src, 64);
-      if (J < 64) {
-        M |= Mj;
-        J = Jj;
-      }
-    }
-    const u64 S = ((u64)readlane((u32)(M >> 32), first) << 32) | readlane((u32)M, first);
-    const bool in_s = (S >> lane) & 1ull;
-    // output position of each chain tag: op + exclusive prefix sum of lengths
-    const u32 lv = in_s ? len : 0u;
-    const u32 t_op = op + dpp_incl_scan(lv) - lv;
-    // writer space and copy offset checks (:761, :1166, :1200, :1410, :1466);
-    // the first failing tag has an exact t_op (every earlier one passed)
-    const bool bad = in_s && (bad_local || expected - t_op < len || (!is_lit && coff - 1u >= t_op));
-    if (__any(bad)) {
-      status = kCorrupt;
-      break;
-    }
-    // 64 KiB output segments for pass 2 (what the reference's encoder emits:
-    // fragments compressed independently, snappy.cc:875-954): no tag may
-    // span a boundary and no copy may reach below its own segment.  A tag
-    // starting exactly at a boundary stores its input offset in the slot's
-    // 4 bytes there; that segment's own output overwrites them in pass 2.
-    if (seg) {
-      const bool span = in_s && len > 0 && ((t_op ^ (t_op + len - 1)) >> 16) != 0;
-      const bool xcopy = in_s && !is_lit && t_op - coff < (t_op & ~0xffffu);
-      if (__any(span || xcopy)) seg = false;
-      if (seg && in_s && t_op != 0 && (t_op & 0xffffu) == 0 && t_op + 4 <= expected)
-        __builtin_memcpy(ob + t_op, &p, 4);
-    }
-    const u32 last = 63u - (u32)__builtin_clzll(S);
-    ip = readlane(nxt, last);
-    op = readlane(t_op + len, last);
-    const u32 wbits = lane == 0 ? (u32)S : (u32)(S >> 32);
-    if (lane < 2 && wbits) bm[(wb >> 5) + lane] = wbits;
-  }
-#endif
   return status;
 }
 
@@ -995,10 +824,6 @@ __global__ __launch_bounds__(4 * 64) void index_big_kernel(
   const u32 n_huge = mode == 2 ? 0u : big_count[8];
   const u32 count = (mode == 1 ? 0u : big_count[0]) + n_huge;
   if (count == 0) return;  // uniform batches: no atomics on the shared counter
-#if FSG_BIG_PRIO
-  // forked path: the longest of these walks is a side stream's critical path
-  if (mode == 2) __builtin_amdgcn_s_setprio(FSG_BIG_PRIO);
-#endif
   for (;;) {  // all-lane atomic: lane 0 adds 1, lane 0's result is the index
     const u32 got = atomicAdd(big_next, lane == 0 ? 1u : 0u);
     const u32 idx = (u32)__builtin_amdgcn_readfirstlane((int)got);
@@ -1545,44 +1370,8 @@ __global__ __launch_bounds__(4 * 64) void chunk_final_kernel(
 // global-to-global, 1 KiB per instruction.
 // ===========================================================================
 namespace {
-#ifndef FSG_FLUSH_LAG
-#define FSG_FLUSH_LAG 1
-#endif
-#ifndef FSG_FAR_SC1
-#define FSG_FAR_SC1 1
-#endif
-#ifndef FSG_NEAR_READY_A
-#define FSG_NEAR_READY_A 1
-#endif
 // A/B knobs of the execution pass
-#ifndef FSG_SLIDE_WAIT
-#define FSG_SLIDE_WAIT 1
-#endif
-#ifndef FSG_EXEC_TAG_VALU
-#define FSG_EXEC_TAG_VALU 0
-#endif
-#ifndef FSG_ROUNDSB_OR
-#define FSG_ROUNDSB_OR 0
-#endif
-#ifndef FSG_RB_MASK
-#define FSG_RB_MASK 0
-#endif
-#ifndef FSG_HOIST_TAG
-#define FSG_HOIST_TAG 0
-#endif
-#ifndef FSG_EARLY_A
-#define FSG_EARLY_A 1
-#endif
-#ifndef FSG_FILL_PAIRS
-#define FSG_FILL_PAIRS 0
-#endif
-#ifndef FSG_PF_POS
-#define FSG_PF_POS 0
-#endif
 // The software-pipelined execution pass (exec6_message; A/B variant).
-#ifndef FSG_EXEC_PIPE
-#define FSG_EXEC_PIPE 0
-#endif
 // Window and kept history: 3 KiB / 1 KiB at 7 waves per SIMD (C3 6.35 ->
 // 6.20 ms against 4 KiB / 2 KiB at 6 waves, A/B on one box; 4 KiB / 1 KiB
 // at 6 waves 6.33, a 256-entry tag ring 7.04).
@@ -1613,20 +1402,8 @@ static_assert(kKeep <= kMaxKeep, "kept history leaves room for one group");
 // ("far copies").  src + 16 <= op <= the slot length
 // (far sources end >= 16 bytes below the window base, which is <= op - 16), so
 // the range check never clips a needed byte.
-#ifdef FSG_DIAG_FAR_FIXED
-// Diagnostic build only (wrong output, timing only): every far load reads one
-// fixed, L2-resident 64-byte line instead of the slot, so the far copies
-// cost their instructions but no memory traffic.
-__device__ u32x4 g_far_line[4];
-#endif
 __device__ __forceinline__ u32x4 far_load(__amdgpu_buffer_rsrc_t r, u32 off) {
-#ifdef FSG_DIAG_FAR_FIXED
-  (void)r;
-  const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc(g_far_line, (short)0, 64, 0x00020000);
-  return __builtin_amdgcn_raw_buffer_load_b128(fr, off & 48u, 0, 0);
-#else
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
-#endif
 }
 
 // One message, executed by the calling wave (see the pass-2 comment above).
@@ -1650,11 +1427,9 @@ __device__ __forceinline__ void exec_message(
   const u32 obal = (u32)(reinterpret_cast<uintptr_t>(ob) & 15);
   // the message's input as a buffer: tag and literal loads need no clamping
   const __amdgpu_buffer_rsrc_t irsrc = msg_rsrc(ib - ibal, ibal + n_in);
-#if FSG_FAR_SC1
   // the message's slot as a buffer: far copies load through it past L1
   const __amdgpu_buffer_rsrc_t orsrc =
       __builtin_amdgcn_make_buffer_rsrc(ob - obal, (short)0, (int)(expected + obal), 0x00020000);
-#endif
 
   if ((bmb & kSingleLiteral) && op1 == expected && op0 == 0) {
     // one literal (checked by pass 1): a straight copy, 4 KiB per step with
@@ -1860,7 +1635,6 @@ __device__ __forceinline__ void exec_message(
     // ---------- slide the window if this group would overrun it
     if (op + tot_len - sbase > kWindow) {
       const int nsb = (int)(((op - keep_hist + obal) & ~15u)) - (int)obal;
-#if FSG_FLUSH_LAG
       // a far piece (source below the new base) may read up to 15 bytes at
       // and above the base, so those must be stored too
       if ((int)flushed < nsb + 16) flush_to((u32)((int)((op + obal) & ~15u) - (int)obal));
@@ -1871,9 +1645,7 @@ __device__ __forceinline__ void exec_message(
       // acknowledged by L2, where the far loads (sc1) are served.  Once per
       // slide (~every 3 KiB of output).
       wait_all_memory();
-#endif
       const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
-#ifndef FSG_KO_SLIDE
       for (u32 k = 0; k < keep; k += 1024) {
         const u32 i = k + 16 * lane;
         u32x4 x = u32x4{0, 0, 0, 0};
@@ -1882,9 +1654,6 @@ __device__ __forceinline__ void exec_message(
         if (i < keep) *reinterpret_cast<u32x4*>(sb + i) = x;
         wave_lds_fence();
       }
-#else
-      (void)shift;
-#endif
       sbase = nsb;
       zero_end = (keep + 15) & ~15u;  // the copied blocks end in zeros past op
     }
@@ -1932,24 +1701,16 @@ __device__ __forceinline__ void exec_message(
     const bool global_src = has && (kT == 0 || (int)src < sbase);
     u32x4 xa = u32x4{0, 0, 0, 0};
     if (global_src)
-#if FSG_FAR_SC1
       xa = kT == 0 ? rsrc_load16(irsrc, src + ibal) : far_load(orsrc, src + obal);
-#else
-      xa = kT == 0 ? rsrc_load16(irsrc, src + ibal) : load16_clamped(ob, src, expected, obal);
-#endif
     if (prio) __builtin_amdgcn_s_setprio(0);
     // the previous group's completed blocks are flushed while these loads are
     // in flight (far sources lie before the window: flushed long ago)
     {
       const int fe = (int)((op + obal) & ~15u) - (int)obal;
-#if FSG_FLUSH_LAG
       // once a wave instruction's worth (1 KiB) is complete: every lane
       // stores a full block.  A slide first flushes what it would drop, so
       // far sources (below the window base) are always in global memory.
       if (fe >= (int)flushed + 1024) flush_to((u32)fe);
-#else
-      if (fe > (int)flushed) flush_to((u32)fe);
-#endif
     }
     if (global_src) {
       if (kT == 2) xa = expand_pattern(xa, offT, sel_tab);
@@ -2096,8 +1857,7 @@ __device__ __forceinline__ void exec5_message(
   u32 bmw = fill_word(scan);
   // the next group's tag bytes: 20 bytes from the dword below the tag
   u32 pf_head = 0xffffffffu, pf_cnt = 0;
-  u32 pf_pos = 0;  // the ring positions the prefetch used (FSG_PF_POS)
-  u32 e_pf = 0;    // their tag-table entries (FSG_HOIST_TAG)
+  u32 pf_pos = 0;  // the ring positions the prefetch used
   u32x4 pd = u32x4{0, 0, 0, 0};
   u32 pd4 = 0;
   auto prefetch = [&](u32 p) {
@@ -2108,7 +1868,6 @@ __device__ __forceinline__ void exec5_message(
 
   auto flush_to = [&](u32 fe) {
     if (fe <= flushed) return;
-#ifndef FSG_KO_FLUSH  // knockout builds (diagnostic, wrong output): time shares
     const int b0 = (int)(((flushed + obal) & ~15u)) - (int)obal;
     for (int blk = b0 + 16 * (int)lane; blk < (int)fe; blk += 1024) {
       const u32 lo = blk < (int)flushed ? flushed : (u32)blk;
@@ -2120,7 +1879,6 @@ __device__ __forceinline__ void exec5_message(
         store_exact(ob + lo, lds_read16(sb + ((int)lo - sbase)), hi - lo);
       }
     }
-#endif
     flushed = fe;
   };
 
@@ -2133,40 +1891,12 @@ __device__ __forceinline__ void exec5_message(
       if (bitbase < ip0) bits &= bitbase + 8 <= ip0 ? 0u : (0xffu << (ip0 - bitbase)) & 0xffu;
       const u32 cnt = __builtin_popcount(bits);
       const u32 incl = dpp_incl_scan(cnt);
-#if FSG_FILL_PAIRS
-      // Two positions per iteration, a lane's bits from the highest down:
-      // with an odd count the first pair's second dword (one past the lane's
-      // last slot) is garbage, which lands on the next lane's first slot (or
-      // past the tail) BEFORE that lane writes it -- its lowest slot is
-      // written in its last pair's first-position store, at this iteration or
-      // later, after every lane's second-position store of the iteration.
-      u32 rem = cnt;
-      const u32 a0 = tail + incl - cnt;
-      while (rem) {
-        const u32 h = 31u - __builtin_clz(bits);
-        const u32 b1 = bits & ~(1u << h);
-        const u32 h2 = b1 ? 31u - __builtin_clz(b1) : 0u;
-        const bool odd = rem & 1u;
-        const u32 at = a0 + rem - (odd ? 1u : 2u);
-        u32* const r0 = ring + (at & (kTagRing - 1));
-        u32* const r1 = ring + ((at + 1) & (kTagRing - 1));
-        // (two stores: the garbage dword first, so the next lane's own store
-        // of that slot -- in this iteration's second store at the latest --
-        // lands after it)
-        *r1 = bitbase + h;
-        wave_lds_fence();
-        *r0 = bitbase + (odd ? h : h2);
-        bits = odd ? b1 : (b1 & ~(1u << h2));
-        rem -= odd ? 1u : 2u;
-      }
-#else
       u32 slot = tail + incl - cnt;
       while (bits) {
         ring[slot & (kTagRing - 1)] = bitbase + __builtin_ctz(bits);
         ++slot;
         bits &= bits - 1;
       }
-#endif
       tail += readlane(incl, 63);
       scan += kFillWords;
       bmw = fill_word(scan);
@@ -2180,35 +1910,14 @@ __device__ __forceinline__ void exec5_message(
     const bool valid = lane < take0;
     // every lane reads the ring and prefetches: a lane past the valid tags
     // reads a stale position, whose buffer loads return message bytes or 0
-#if FSG_HOIST_TAG
-    // the tag-table entry of the prefetched tags was read at the end of the
-    // last group (e_pf) unless a fill since added tags: then re-prefetch
-    const bool pf_ok = pf_head == head && pf_cnt >= take0;
-#endif
-#if FSG_PF_POS || FSG_HOIST_TAG
-    // the prefetch's ring positions are this group's unless a fill added
-    // tags after it: then read the ring and prefetch again
-    u32 pos = pf_pos;
-    if (pf_head != head || pf_cnt < take0) {
-      pos = ring[(head + lane) & (kTagRing - 1)];
-      prefetch(pos);
-    }
-#else
     const u32 pos = ring[(head + lane) & (kTagRing - 1)];
     if (pf_head != head || pf_cnt < take0) prefetch(pos);
-#endif
     if (prio) __builtin_amdgcn_s_setprio(1);
 
     // ---------- decode one tag per lane (checked by pass 1)
     const u32 s = (pos + ibal) & 3u;
     const u32 c = __builtin_amdgcn_alignbyte(pd[1], pd[0], s) & 0xffu;
-#if FSG_EXEC_TAG_VALU
-    const u32 e = exec_tag_entry(c);
-#elif FSG_HOIST_TAG
-    const u32 e = pf_ok ? e_pf : tagtab[c];
-#else
     const u32 e = tagtab[c];
-#endif
     // bytes pos+1 .. pos+16 (a short literal's bytes; a copy's offset bytes)
     const bool q = s == 3;
     const u32 w0 = q ? pd[1] : pd[0], w1 = q ? pd[2] : pd[1], w2 = q ? pd[3] : pd[2];
@@ -2290,11 +1999,8 @@ __device__ __forceinline__ void exec5_message(
     if (op + tot_len - sbase > kWindow) {
       const int nsb = (int)(((op - keep_hist + obal) & ~15u)) - (int)obal;
       if ((int)flushed < nsb + 16) flush_to((u32)((int)((op + obal) & ~15u) - (int)obal));
-#if FSG_SLIDE_WAIT
       wait_all_memory();
-#endif
       const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
-#ifndef FSG_KO_SLIDE
       for (u32 k = 0; k < keep; k += 1024) {
         const u32 i = k + 16 * lane;
         u32x4 x = u32x4{0, 0, 0, 0};
@@ -2303,9 +2009,6 @@ __device__ __forceinline__ void exec5_message(
         if (i < keep) *reinterpret_cast<u32x4*>(sb + i) = x;
         wave_lds_fence();
       }
-#else
-      (void)shift;
-#endif
       sbase = nsb;
       zero_end = (keep + 15) & ~15u;
     }
@@ -2321,16 +2024,11 @@ __device__ __forceinline__ void exec5_message(
         pf_cnt = ncnt;
       }
       while (op + tot_len + 20 - sbase > zero_end) {
-#ifndef FSG_KO_ZERO
         zero_from(zero_end);
-#endif
         zero_end += 1024;
       }
       wave_lds_fence();
     };
-#if !FSG_EARLY_A
-    prefetch_next_and_zero();
-#endif
 
     STAMP(2);
     // ---------- chunks: a literal's all come in round A (registers for
@@ -2345,18 +2043,13 @@ __device__ __forceinline__ void exec5_message(
     // those whose source ends at or below the group's first output byte op
     // (near-ready: final window bytes, read from LDS) -- none for a pattern.
     // A near-ready chunk would run in the first round B anyway; in round A it
-    // is one OR store among the group's, not a read-modify-write of its own
-    // (FSG_NEAR_READY_A=0: rounds B take them, as before).
+    // is one OR store among the group's, not a read-modify-write of its own.
     const u32 below = (u32)(sbase - (int)src);  // > 0 as int: far
     const u32 kfar = (int)below > 0 ? ((below - 1) >> 4) + 1 : 0u;
-#if FSG_NEAR_READY_A
     // chunk k's source ends at src + min(16 (k + 1), len): <= op for the
     // first (op - src) / 16 chunks, or all of them when src + len <= op
     const u32 kready = src + len <= op ? nch : (src < op ? (op - src) >> 4 : 0u);
     const u32 klead = kfar > kready ? kfar : kready;
-#else
-    const u32 klead = kfar;
-#endif
     const u32 kc = pat ? 0u : (klead < nch ? klead : nch);
     const u32 kf = fits ? (is_lit ? nch : kc) : 0u;
     const bool reg0 = is_lit && nb == 0;
@@ -2370,10 +2063,8 @@ __device__ __forceinline__ void exec5_message(
         const u32 a = (src + 16 * k + ibal) & ~3u;
         d = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
         d4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
-#if FSG_NEAR_READY_A
       } else if (k >= kfar) {  // near-ready: final bytes below op in the window
         d = lds_read16(sb + ((int)(src + 16 * k) - sbase));
-#endif
       } else {
         d = far_load(orsrc, src + 16 * k + obal);
       }
@@ -2384,20 +2075,14 @@ __device__ __forceinline__ void exec5_message(
     };
     u32x4 a0 = xr, a1 = u32x4{0, 0, 0, 0};
     u32 a0e = 0, a1e = 0;
-#ifndef FSG_KO_LOADS
     if (kf > 0 && !reg0) gload(0, a0, a0e);
-#endif
     const u64 m1 = __ballot(kf > 1);
-#ifndef FSG_KO_LOADS
     if (m1 && kf > 1) gload(1, a1, a1e);
-#endif
-#if FSG_EARLY_A
     // (the round-A loads go out before the next group's ring read and tag
     // prefetch and the window zeroing: their latency is the group's longest
     // wait; the near-ready LDS reads above read bytes below op, which the
     // zeroing (from zero_end >= op) does not touch)
     prefetch_next_and_zero();
-#endif
     if (prio) __builtin_amdgcn_s_setprio(0);
     STAMP(3);
     {  // the previous groups' completed blocks, while the loads are in flight
@@ -2406,12 +2091,8 @@ __device__ __forceinline__ void exec5_message(
     }
     STAMP(4);
     const u32 wa = (u32)((int)t_op - sbase);
-#ifdef FSG_KO_A
-    if (m1 && false) {
-#else
     if (kf > 0) or_store(sb, wa, shf(a0, a0e, reg0 ? 0u : sh), len < 16 ? len : 16u, mtab);
     if (m1) {
-#endif
       if (kf > 1) or_store(sb, wa + 16, shf(a1, a1e, sh), len - 16 < 16 ? len - 16 : 16u, mtab);
       // chunks 2-3 (literals and far copies of 33..64 bytes: rare) reuse the
       // registers, one more round trip
@@ -2443,41 +2124,22 @@ __device__ __forceinline__ void exec5_message(
     bool pf = pat;
     u32 ne = rem ? (pf ? cw : sw + n) : 0xffffffffu;
     u64 pend = __ballot(rem > 0);
-#ifdef FSG_DBG_NOB  // diagnostic builds only (instruction accounting): wrong output
-    pend = 0;
-#endif
-#if FSG_ROUNDS_V2
     // Most groups (~90% on text) hold no pattern copy: their rounds run a
     // loop with no per-lane pattern state (the general loop below costs ~6
     // more instructions per round).
     if (!__ballot(pat && rem > 0)) {
-#if FSG_RB_MASK
-      // the mask of the lane's last chunk, once (its other chunks are whole)
-      const u32x4 mk_last = mtab[rem ? ((rem - 1) & 15u) + 1u : 0u];
-#endif
       while (pend) {
         const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
         if (ne <= W) {
           const u32x4 x = lds_read16(sb + sw);
-#if FSG_ROUNDSB_OR
-          // OR into the zeroed window (the chunk's own bytes are still zero)
-          or_store(sb, cw, x, n, mtab);
-#else
           const u32x4 o = lds_read16(sb + cw);
-#if FSG_RB_MASK
-          const bool whole = rem > 16;
-          const u32x4 mk = u32x4{whole ? ~0u : mk_last[0], whole ? ~0u : mk_last[1], whole ? ~0u : mk_last[2],
-                                 whole ? ~0u : mk_last[3]};
-#else
           const u32x4 mk = mtab[n];
-#endif
           u32x4 y;
           y[0] = (x[0] & mk[0]) | (o[0] & ~mk[0]);
           y[1] = (x[1] & mk[1]) | (o[1] & ~mk[1]);
           y[2] = (x[2] & mk[2]) | (o[2] & ~mk[2]);
           y[3] = (x[3] & mk[3]) | (o[3] & ~mk[3]);
           __builtin_memcpy(sb + cw, &y, 16);
-#endif
           rem -= n;
           cw += n;
           sw += n;
@@ -2488,7 +2150,6 @@ __device__ __forceinline__ void exec5_message(
         pend = __ballot(rem > 0);
       }
     }
-#endif
     while (pend) {
       const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
       if (ne <= W) {
@@ -2514,11 +2175,6 @@ __device__ __forceinline__ void exec5_message(
     }
     op += tot_len;
     head += k_tags;
-#if FSG_HOIST_TAG
-    // the next group's tag-table entries, now: the prefetched tag bytes have
-    // long landed, and the read's latency overlaps the loop's head
-    e_pf = tagtab[__builtin_amdgcn_alignbyte(pd[1], pd[0], (pf_pos + ibal) & 3u) & 0xffu];
-#endif
     STAMP(6);
   }
   if (op != op1) {  // the stream ended early (snappy.cc:858-868)
@@ -2532,381 +2188,6 @@ __device__ __forceinline__ void exec5_message(
 #endif
 }
 
-#if FSG_EXEC_PIPE
-// ===========================================================================
-// Software-pipelined execution pass (A/B variant, -DFSG_EXEC_PIPE=1; VERDICT
-// r4 item 1): the same group rules as exec5_message, but the NEXT group's
-// front -- ring read, tag decode, prefix sum, writer checks, chunk
-// classification, round-A loads, the prefetch of the group after it and the
-// window zeroing -- is issued before this group's rounds B, so its loads are
-// in flight while the rounds run.  The early front is taken only when it
-// needs no ring refill, no window slide and no long literal (else the group
-// goes the ordinary way), and it treats only output below this group's first
-// byte as final (its near-ready chunks: bytes this group's rounds B have not
-// written yet wait for its own rounds B).  Far loads stay safe: every far
-// source lies below the window base, which the last slide flushed and waited
-// for (section 4, "far copies").
-// ===========================================================================
-__device__ __forceinline__ void exec6_message(
-    u32 m, const u8* __restrict__ in, const u64* __restrict__ in_off,
-    const u32* __restrict__ in_len, u8* out, const u64* __restrict__ out_off,
-    const u32* __restrict__ out_len, i32* __restrict__ status, const u32* __restrict__ bm_base,
-    const u32* __restrict__ bitmap, u32* ring, const u32* tagtab, u8* sb, const u32x4* sel_tab,
-    const u32x4* mtab, u32 lane, i32 st, u32 ip0, u32 op0, u32 op1, bool prio, u32 keep_hist) {
-  const u32 bmb = bm_base[m];
-  const u32 n_in = in_len[m];
-  const u32 expected = out_len[m];
-  const u8* ib = in + in_off[m];
-  u8* ob = out + out_off[m];
-  if (st != kOk) return;
-  const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
-  const u32 obal = (u32)(reinterpret_cast<uintptr_t>(ob) & 15);
-  const __amdgpu_buffer_rsrc_t irsrc = msg_rsrc(ib - ibal, ibal + n_in);
-  const __amdgpu_buffer_rsrc_t orsrc =
-      __builtin_amdgcn_make_buffer_rsrc(ob - obal, (short)0, (int)(expected + obal), 0x00020000);
-
-  if ((bmb & kSingleLiteral) && op1 == expected && op0 == 0) {
-    const u32 S = bmb & ~kSingleLiteral;
-    for (u32 k0 = 0; k0 < expected; k0 += 4096) {
-      Raw16 x[4];
-#pragma unroll
-      for (u32 r = 0; r < 4; ++r) x[r] = raw_load16(irsrc, S + k0 + 1024 * r + lane * 16 + ibal);
-#pragma unroll
-      for (u32 r = 0; r < 4; ++r) {
-        const u32 k = k0 + 1024 * r + lane * 16;
-        if (k < expected) store_exact(ob + k, shifted16(x[r]), expected - k < 16 ? expected - k : 16u);
-      }
-    }
-    return;
-  }
-  const u32* bm = bitmap + bmb;
-  const u32 nwords = (n_in + 31) >> 5;
-
-  u32 head = 0, tail = 0, scan = ip0 >> 5, op = op0;
-  int sbase = (int)((op0 + obal) & ~15u) - (int)obal;
-  u32 flushed = op0;
-  auto zero_from = [&](u32 from) {
-    const u32 i = from + 16 * lane;
-    if (i < kWindow + 32) *reinterpret_cast<u32x4*>(sb + i) = u32x4{0, 0, 0, 0};
-  };
-  zero_from(0);
-  u32 zero_end = 1024;
-  wave_lds_fence();
-  auto fill_word = [&](u32 sc) -> u32 {
-    const u32 wi = sc + (lane >> 2);
-    return (lane < 4 * kFillWords && wi < nwords) ? bm[wi] : 0u;
-  };
-  u32 bmw = fill_word(scan);
-  u32 pf_head = 0xffffffffu, pf_cnt = 0;
-  u32x4 pd = u32x4{0, 0, 0, 0};
-  u32 pd4 = 0;
-  auto prefetch = [&](u32 p) {
-    const u32 a = (p + ibal) & ~3u;
-    pd = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
-    pd4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
-  };
-  auto flush_to = [&](u32 fe) {
-    if (fe <= flushed) return;
-    const int b0 = (int)(((flushed + obal) & ~15u)) - (int)obal;
-    for (int blk = b0 + 16 * (int)lane; blk < (int)fe; blk += 1024) {
-      const u32 lo = blk < (int)flushed ? flushed : (u32)blk;
-      const u32 hi = blk + 16 < (int)fe ? (u32)(blk + 16) : fe;
-      if (hi - lo == 16) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(sb + (blk - sbase));
-        __builtin_memcpy(ob + blk, &v, 16);
-      } else {
-        store_exact(ob + lo, lds_read16(sb + ((int)lo - sbase)), hi - lo);
-      }
-    }
-    flushed = fe;
-  };
-
-  // ---- the group state, loop-carried: the front of the group at `head`
-  // (decoded, scanned, classified, round-A loads in flight) when `have`
-  bool have = false;
-  u32 len = 0, off = 0, src = 0, t_op = 0, kf = 0, sh = 0, kfar = 0, k_tags = 0, tot_len = 0, lsrc = 0;
-  bool is_lit = false, reg0 = false, pat = false, fits = false;
-  u64 m1 = 0;
-  u32x4 a0 = u32x4{0, 0, 0, 0}, a1 = u32x4{0, 0, 0, 0};
-  u32 a0e = 0, a1e = 0;
-  auto gload = [&](u32 k, u32x4& d, u32& d4) {
-    if (is_lit) {
-      const u32 a = (src + 16 * k + ibal) & ~3u;
-      d = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
-      d4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
-    } else if (k >= kfar) {
-      d = lds_read16(sb + ((int)(src + 16 * k) - sbase));
-    } else {
-      d = far_load(orsrc, src + 16 * k + obal);
-    }
-  };
-  // The front of the group at ghead whose first output byte is gop; output
-  // below `ready` is final.  Early: no slide, and the prefetch must be this
-  // group's.  Returns 0 done, 1 a long literal first (nothing changed), 2 a
-  // slide needed (early only), 3 corrupt (status written), 4 no prefetch.
-  auto front = [&](u32 ghead, u32 gop, u32 ready, bool early) -> int {
-    const u32 avail = tail - ghead;
-    const u32 take0 = avail < 64 ? avail : 64u;
-    const bool valid = lane < take0;
-    const bool pf_ok = pf_head == ghead && pf_cnt >= take0;
-    if (early && !pf_ok) return 4;
-    const u32 pos = ring[(ghead + lane) & (kTagRing - 1)];
-    if (!pf_ok) prefetch(pos);
-    if (prio) __builtin_amdgcn_s_setprio(1);
-    const u32 s = (pos + ibal) & 3u;
-    const u32 c = __builtin_amdgcn_alignbyte(pd[1], pd[0], s) & 0xffu;
-    const u32 e = tagtab[c];
-    const bool q = s == 3;
-    const u32 w0 = q ? pd[1] : pd[0], w1 = q ? pd[2] : pd[1], w2 = q ? pd[3] : pd[2];
-    const u32 w3 = q ? pd4 : pd[3];
-    const u32 b = (s + 1) & 3u;
-    const u32x4 xr = u32x4{__builtin_amdgcn_alignbyte(w1, w0, b), __builtin_amdgcn_alignbyte(w2, w1, b),
-                           __builtin_amdgcn_alignbyte(w3, w2, b), __builtin_amdgcn_alignbyte(pd4, w3, b)};
-    const u32 val = xr[0] & (0xffffffffu >> (e & 31u));
-    const bool lit = e & 64u;
-    const u32 ln = (e & 32u) ? val + 1u : (e >> 8) & 0x7fu;
-    const u32 nb = (e >> 16) & 7u;
-    const u64 bigm = __ballot(valid && lit && ln > 64);
-    if (bigm & 1ull) {
-      len = ln;
-      lsrc = pos + 1 + nb;
-      return 1;
-    }
-    is_lit = lit;
-    len = ln;
-    off = val + (e >> 20);
-    lsrc = pos + 1 + nb;
-    const u32 take = bigm ? (u32)__builtin_ctzll(bigm) : take0;
-    const bool v = lane < take;
-    const u32 lv = v ? len : 0u;
-    const u32 incl = dpp_incl_scan(lv);
-    t_op = gop + incl - lv;
-    fits = v && incl <= kGroupBytes && t_op < op1;
-    k_tags = (u32)__builtin_popcountll(__ballot(fits));
-    tot_len = readlane(incl, k_tags - 1);
-    if (__any(fits && (len > op1 - t_op || (!is_lit && (off == 0 || off > t_op - op0))))) {
-      if (lane == 0) status[m] = kCorrupt;
-      return 3;
-    }
-    if (gop + tot_len - sbase > kWindow) {
-      if (early) return 2;
-      const int nsb = (int)(((gop - keep_hist + obal) & ~15u)) - (int)obal;
-      if ((int)flushed < nsb + 16) flush_to((u32)((int)((gop + obal) & ~15u) - (int)obal));
-      wait_all_memory();
-      const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)gop - nsb);
-      for (u32 k = 0; k < keep; k += 1024) {
-        const u32 i = k + 16 * lane;
-        u32x4 x = u32x4{0, 0, 0, 0};
-        if (i < keep) x = *reinterpret_cast<const u32x4*>(sb + shift + i);
-        wave_lds_fence();
-        if (i < keep) *reinterpret_cast<u32x4*>(sb + i) = x;
-        wave_lds_fence();
-      }
-      sbase = nsb;
-      zero_end = (keep + 15) & ~15u;
-    }
-    src = is_lit ? lsrc : t_op - off;
-    const u32 nch = (len + 15) >> 4;
-    pat = !is_lit && off < 16 && off < len;
-    const u32 below = (u32)(sbase - (int)src);
-    kfar = (int)below > 0 ? ((below - 1) >> 4) + 1 : 0u;
-    const u32 kready = src + len <= ready ? nch : (src < ready ? (ready - src) >> 4 : 0u);
-    const u32 klead = kfar > kready ? kfar : kready;
-    const u32 kc = pat ? 0u : (klead < nch ? klead : nch);
-    kf = fits ? (is_lit ? nch : kc) : 0u;
-    reg0 = is_lit && nb == 0;
-    sh = is_lit ? (src + ibal) & 3u : 0u;
-    a0 = xr;
-    a1 = u32x4{0, 0, 0, 0};
-    a0e = 0;
-    a1e = 0;
-    if (kf > 0 && !reg0) gload(0, a0, a0e);
-    m1 = __ballot(kf > 1);
-    if (m1 && kf > 1) gload(1, a1, a1e);
-    {  // the next group's tag bytes; the window zeroed ahead
-      const u32 nh = ghead + k_tags;
-      const u32 na = tail - nh;
-      pf_head = nh;
-      pf_cnt = na < 64 ? na : 64u;
-      prefetch(ring[(nh + lane) & (kTagRing - 1)]);
-      while (gop + tot_len + 20 - sbase > zero_end) {
-        zero_from(zero_end);
-        zero_end += 1024;
-      }
-      wave_lds_fence();
-    }
-    if (prio) __builtin_amdgcn_s_setprio(0);
-    return 0;
-  };
-  auto shf = [&](const u32x4& d, u32 d4, u32 t) {
-    return u32x4{__builtin_amdgcn_alignbyte(d[1], d[0], t), __builtin_amdgcn_alignbyte(d[2], d[1], t),
-                 __builtin_amdgcn_alignbyte(d[3], d[2], t), __builtin_amdgcn_alignbyte(d4, d[3], t)};
-  };
-
-  for (;;) {
-    if (!have) {
-      if (tail - head < 2 * kMaxPieces && scan < nwords) {
-        if (prio) __builtin_amdgcn_s_setprio(1);
-        u32 bits = (bmw >> (8 * (lane & 3))) & 0xffu;
-        const u32 bitbase = (scan + (lane >> 2)) * 32 + 8 * (lane & 3);
-        if (bitbase < ip0) bits &= bitbase + 8 <= ip0 ? 0u : (0xffu << (ip0 - bitbase)) & 0xffu;
-        const u32 cnt = __builtin_popcount(bits);
-        const u32 incl = dpp_incl_scan(cnt);
-        u32 slot = tail + incl - cnt;
-        while (bits) {
-          ring[slot & (kTagRing - 1)] = bitbase + __builtin_ctz(bits);
-          ++slot;
-          bits &= bits - 1;
-        }
-        tail += readlane(incl, 63);
-        scan += kFillWords;
-        bmw = fill_word(scan);
-        wave_lds_fence();
-        continue;
-      }
-      if (tail == head || op >= op1) break;
-      const int r = front(head, op, op, false);
-      if (r == 3) return;
-      if (r == 1) {
-        // ---------- long literal: written straight to the slot by the
-        // whole wave; the window restarts behind it (as exec5_message)
-        const u32 L = readlane(len, 0), S = readlane(lsrc, 0);
-        if ((u64)op + L > op1) {
-          if (lane == 0) status[m] = kCorrupt;
-          return;
-        }
-        flush_to(op);
-        for (u32 k0 = 0; k0 < L; k0 += 4096) {
-          Raw16 x[4];
-#pragma unroll
-          for (u32 r2 = 0; r2 < 4; ++r2) x[r2] = raw_load16(irsrc, S + k0 + 1024 * r2 + lane * 16 + ibal);
-#pragma unroll
-          for (u32 r2 = 0; r2 < 4; ++r2) {
-            const u32 k = k0 + 1024 * r2 + lane * 16;
-            if (k < L) store_exact(ob + op + k, shifted16(x[r2]), L - k < 16 ? L - k : 16u);
-          }
-        }
-        op += L;
-        flushed = op;
-        sbase = (int)((op + obal) & ~15u) - (int)obal - 16;
-        zero_from(0);
-        zero_end = 1024;
-        wave_lds_fence();
-        if (lane < 2) {
-          const u32 lo = (u32)sbase + 16 * lane;
-          if (lo < op) {
-            const u32 cnt = op - lo < 16 ? op - lo : 16u;
-            store_exact(sb + 16 * lane, rsrc_load16(irsrc, S + L - (op - lo) + ibal), cnt);
-          }
-        }
-        wave_lds_fence();
-        head += 1;
-        pf_head = 0xffffffffu;
-        if (head == tail) {
-          const u32 nw = (S + L) >> 5;
-          if (nw > scan) {
-            scan = nw;
-            bmw = fill_word(scan);
-          }
-        }
-        continue;
-      }
-    }
-    have = false;
-    {  // the previous groups' completed blocks, while the loads are in flight
-      const int fe = (int)((op + obal) & ~15u) - (int)obal;
-      if (fe >= (int)flushed + 1024) flush_to((u32)fe);
-    }
-    const u32 wa = (u32)((int)t_op - sbase);
-    if (kf > 0) or_store(sb, wa, shf(a0, a0e, reg0 ? 0u : sh), len < 16 ? len : 16u, mtab);
-    if (m1) {
-      if (kf > 1) or_store(sb, wa + 16, shf(a1, a1e, sh), len - 16 < 16 ? len - 16 : 16u, mtab);
-      if (__ballot(kf > 2)) {
-        if (kf > 2) gload(2, a0, a0e);
-        if (kf > 3) gload(3, a1, a1e);
-        if (kf > 2) or_store(sb, wa + 32, shf(a0, a0e, sh), len - 32 < 16 ? len - 32 : 16u, mtab);
-        if (kf > 3) or_store(sb, wa + 48, shf(a1, a1e, sh), len - 48, mtab);
-      }
-    }
-    wave_lds_fence();
-    // ---------- rounds B state of this group (as exec5_message)
-    u32 rem = (fits && kf < ((len + 15) >> 4)) ? len - 16 * kf : 0u;
-    u32 cw = (u32)((int)t_op - sbase) + 16 * kf;
-    u32 sw = (u32)((int)src - sbase) + 16 * kf;
-    const bool gpat = pat;
-    const u32 goff = off;
-    const u32 stp = gpat ? pat_step(goff) : 16u;
-    u32 n = rem < stp ? rem : stp;
-    bool pf = gpat;
-    u32 ne = rem ? (pf ? cw : sw + n) : 0xffffffffu;
-    u64 pend = __ballot(rem > 0);
-    const u32 g_tot = tot_len, g_k = k_tags;
-    // ---------- the next group's front, before this group's rounds B
-    {
-      const u32 nh = head + g_k, nop = op + g_tot;
-      if ((tail - nh >= 2 * kMaxPieces || scan >= nwords) && tail > nh && nop < op1) {
-        const int r = front(nh, nop, op, true);
-        if (r == 3) return;
-        have = r == 0;
-      }
-    }
-    // ---------- rounds B (as exec5_message)
-    if (!__ballot(gpat && rem > 0)) {
-      while (pend) {
-        const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
-        if (ne <= W) {
-          const u32x4 x = lds_read16(sb + sw);
-          const u32x4 o = lds_read16(sb + cw);
-          const u32x4 mk = mtab[n];
-          u32x4 y;
-          y[0] = (x[0] & mk[0]) | (o[0] & ~mk[0]);
-          y[1] = (x[1] & mk[1]) | (o[1] & ~mk[1]);
-          y[2] = (x[2] & mk[2]) | (o[2] & ~mk[2]);
-          y[3] = (x[3] & mk[3]) | (o[3] & ~mk[3]);
-          __builtin_memcpy(sb + cw, &y, 16);
-          rem -= n;
-          cw += n;
-          sw += n;
-          n = rem < 16u ? rem : 16u;
-          ne = rem ? sw + n : 0xffffffffu;
-        }
-        wave_lds_fence();
-        pend = __ballot(rem > 0);
-      }
-    }
-    while (pend) {
-      const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
-      if (ne <= W) {
-        u32x4 x = lds_read16(sb + sw);
-        if (pf) x = expand_pattern(x, goff, sel_tab);
-        const u32x4 o = lds_read16(sb + cw);
-        const u32x4 mk = mtab[n];
-        u32x4 y;
-        y[0] = (x[0] & mk[0]) | (o[0] & ~mk[0]);
-        y[1] = (x[1] & mk[1]) | (o[1] & ~mk[1]);
-        y[2] = (x[2] & mk[2]) | (o[2] & ~mk[2]);
-        y[3] = (x[3] & mk[3]) | (o[3] & ~mk[3]);
-        __builtin_memcpy(sb + cw, &y, 16);
-        rem -= n;
-        cw += n;
-        sw = gpat ? cw - stp : sw + n;
-        pf = false;
-        n = rem < stp ? rem : stp;
-        ne = rem ? sw + n : 0xffffffffu;
-      }
-      wave_lds_fence();
-      pend = __ballot(rem > 0);
-    }
-    op += g_tot;
-    head += g_k;
-  }
-  if (op != op1) {  // the stream ended early (snappy.cc:858-868)
-    if (lane == 0) status[m] = kCorrupt;
-    return;
-  }
-  flush_to(op1);
-}
-#endif
 
 // 7 waves per SIMD by default (FSG_EXEC_WAVES; 72 VGPRs, 22.2 KB of LDS per
 // block with the 3 KiB window: C3 6.35 -> 6.20 ms against 6 waves with a
@@ -2946,13 +2227,8 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
   // one message (or segment) with the pass-2 variant V
   auto run = [&](u32 m, u32* ring, u8* pmap, u8* sb, u32 lane, i32 st, u32 ip0, u32 op0, u32 op1) {
     if constexpr (V == 5)
-#if FSG_EXEC_PIPE
-      exec6_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, tagtab,
-                    sb, sel_tab, mask_tab, lane, st, ip0, op0, op1, prio != 0, keep_hist);
-#else
       exec5_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, tagtab,
                     sb, sel_tab, mask_tab, lane, st, ip0, op0, op1, prio != 0, keep_hist);
-#endif
     else
       exec_message(m, in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, ring, pmap,
                    sb, sel_tab, mask_tab, lane, st, ip0, op0, op1, prio != 0, keep_hist);
@@ -2978,8 +2254,8 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
       // the messages in walk order (forked path): positions [lo, hi) of
       // walk_perm -- part 1 / 2 the larger / smaller bodies, 3 all of them
       const u32 n_walk = walk_hist[2 * kWalkClasses];
-      // (split_class bits 8-15: the tiny-body pass's first class, whose
-      // positions on are not executed here)
+      // (split_class bits 8-15: the first class another pass takes, whose
+      // positions on are not executed here; no pass sets it now)
       const u32 tcls = split_class >> 8;
       const u32 split = walk_hist[kWalkClasses + (split_class & 0xffu)];
       const u32 t_hi = tcls ? walk_hist[kWalkClasses + tcls] : n_walk;
@@ -3225,13 +2501,9 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   // lists between them are 20 B per message (A/B: C2 0.159 -> 0.157 ms, C3
   // and CM neutral; a zeroing kernel in place of the runtime fill makes the
   // next index pass place its one-wave workgroups unevenly: C3 +0.27 ms)
-#if FSG_BITMAP_NOZERO
   // counters and lists only: the passes that write the bitmap store every
   // word the execution pass reads (C3: an 80 us fill of 267 MB saved)
   hipError_t e = hipMemsetAsync(w, 0, 256 + kListBases * base_bytes, stream);
-#else
-  hipError_t e = hipMemsetAsync(w, 0, 256 + kListBases * base_bytes + cap_words * 4, stream);
-#endif
   if (e != hipSuccess) return e;
   // Large-message threshold: 4x the batch's mean compressed size (estimated
   // from the workspace, which callers size from the packed input), clamped
@@ -3265,17 +2537,12 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
   const u32 split_mode = (u32)opt(kOptSplitWalk);
   const bool split_walk = split_mode == 1;
   const u32 kSplitClass = (u32)opt(kOptSplitClass) % kWalkClasses;
-  // The tiny-body pass (snappy_decode_tiny.hip): walk classes >= kTinyClass
-  // (compressed < 512 B) decoded one body per lane in LDS, in mode 3 only;
-  // the lane walk and the small bodies' execution stop at its first class.
-  const bool tiny = opt(kOptTinyPass) != 0 && split_mode == 3 && kSplitClass < kTinyClass;
-  const u32 tiny_bits = tiny ? kTinyClass << 8 : 0u;
   auto launch_index = [&](bool planned, hipStream_t st = nullptr, u32 part = 0) -> hipError_t {
     if (planned)
       index_kernel<true><<<idx_blocks, 64 * kIdxWaves, 0, st ? st : stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
           cap_words, big_count, big_list, big_threshold, kWalkOrder ? walk_perm : nullptr, walk_hist, part,
-          kSplitClass | tiny_bits);
+          kSplitClass);
     else if (two && kLeanWalk)
       index_kernel<false, true><<<idx_blocks, 64 * kIdxWaves, idx_lean_lds_bytes(), stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
@@ -3420,7 +2687,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
         in, in_off, in_len, n_msgs, out, out_off, out_len, status, bm_base, bitmap,
         reinterpret_cast<const u32*>(seg_list), set0.seg_count, whole_list, set0.whole_count, set0.exec_next,
         0u, big_threshold, 0u, keep_hist, grid < small_blocks ? grid : 0u, part ? walk_perm : nullptr,
-        part ? walk_hist : nullptr, part, kSplitClass | tiny_bits);
+        part ? walk_hist : nullptr, part, kSplitClass);
     return hipGetLastError();
   };
   SideStream* side = fork ? side_stream() : nullptr;
@@ -3464,12 +2731,6 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
       if ((e = launch_small(stream, 2u)) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(stream, side->join3, 0)) != hipSuccess) return e;
     } else {
-      if (tiny && kWalkOrder) {
-        // the tiny bodies first: one lane each, the walk skips them
-        if ((e = launch_tiny(in, in_off, in_len, out, out_off, out_len, status, walk_perm, walk_hist,
-                             kWalkClasses, kTinyClass, kTinyBlocks, stream)) != hipSuccess)
-          return e;
-      }
       if ((e = launch_index(true)) != hipSuccess) return e;
       if (kWalkOrder && split_mode == 2) {
         if ((e = launch_small(stream, 3u)) != hipSuccess) return e;
@@ -3500,9 +2761,6 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
         big_blocks, big_threshold, kPrio, keep_hist, 0u, nullptr, nullptr, 0u, 0u);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  // Diagnostic only (option diag_no_tail 1): skip this pass to trace the
-  // launch-order effect; wrong for kNeedFallback messages.
-  if (opt(kOptDiagNoTail) == 1) return hipSuccess;
   fallback_kernel<<<(n_msgs + 63) / 64, 64, 0, stream>>>(in, in_off, in_len, n_msgs, out, out_off,
                                                          out_len, status, flags);
   return hipGetLastError();

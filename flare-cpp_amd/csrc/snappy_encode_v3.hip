@@ -618,7 +618,6 @@ __global__ void encode_wave_kernel(const u8* __restrict__ in, const u64* __restr
                                    const u64* __restrict__ out_off, u32* __restrict__ out_len,
                                    i32* __restrict__ status, u32* __restrict__ ctr, const u32* __restrict__ items,
                                    u32* __restrict__ sizes, u32 region_cap, u32 share_permille, u64 all_bytes);
-size_t encode_wave_static_lds_bytes();
 
 // Per-device side stream for the wave encoder (created on first use; nullptr:
 // the wave encoder runs on the caller's stream before the lanes).
@@ -694,7 +693,7 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
   if (wave_min) {
     const u32 cap = max_in_len > kBlockSize ? kBlockSize : max_in_len;
     const u32 lds = table_size_for(cap) * 2;
-    u32 per_cu = (160u * 1024u) / (lds + (u32)encode_wave_static_lds_bytes());
+    u32 per_cu = (160u * 1024u) / lds;
     const i64 pc_opt = opt(kOptEncodeWavePerCu);
     if (pc_opt > 0 && (u64)pc_opt < per_cu) per_cu = (u32)pc_opt;
     u32 waves = 256u * (per_cu ? per_cu : 1u);

@@ -49,38 +49,6 @@ namespace {
 
 constexpr u32 kPredNone = 0xff, kPredUnknown = 0xfe;
 
-// The event loop's fast path (see wave_fragment): 2 = each lane precomputes
-// the event of a post-copy arrival at its position, and the walk follows
-// them; 1 = the same rules evaluated event by event; 0 = the general path
-// only (A/B builds).
-#ifndef FSG_WENC_FAST
-#define FSG_WENC_FAST 2
-#endif
-// Output bytes stored straight to global memory (no LDS staging ring) and
-// the in-block predecessors found without a scratch array (see the pred
-// rounds), so the table is the wave's only LDS (four 32 KiB tables stay
-// resident per CU either way; the gain is the ring's round trips).  0 = the
-// staging ring and the pred scratch (A/B builds).
-#ifndef FSG_WENC_DIRECT
-#define FSG_WENC_DIRECT 1
-#endif
-// With FSG_WENC_FAST 2: the fast events' chains resolved for every lane at
-// once by pointer doubling after the precomputation, so an arrival takes its
-// whole chain in a few readlanes; 0 = the walk, one readlane chain per event.
-#ifndef FSG_WENC_CHAIN
-#define FSG_WENC_CHAIN 0
-#endif
-// Input loads two blocks ahead instead of one (A/B).
-#ifndef FSG_WENC_AHEAD2
-#define FSG_WENC_AHEAD2 0
-#endif
-// (ds_write_b8 into the staging ring, or a byte store to the output)
-#if FSG_WENC_DIRECT
-#define OUTB(i) obase[(i)]
-#else
-#define OUTB(i) stg[(i) & 511]
-#endif
-
 // Diagnostic build only (-DFSG_STAMPS): per-phase cycle totals of the wave
 // encoder, summed over waves (fsg_debug_wstamps).
 #ifdef FSG_STAMPS
@@ -164,15 +132,14 @@ __device__ __forceinline__ u32 copy_tag(u32 offset, u32 len, u32* nb) {
 // fragment's first byte.  Output from obase; returns the end, or nullptr if a
 // staged region (op_lim != nullptr) would overflow.
 //
-// Output goes through a 512-byte LDS ring (stg): tag bytes and short literals
-// are written there (one ds_write_b8 per lane), and a block's output is
-// stored to global memory at the start of the NEXT block, after that block's
-// input waits: the waits then never cover young stores (a wave's loads and
-// stores share one counter, so a wait for a load issued before a burst of
-// stores would wait for the stores too).  Long literals and long copies go
-// straight to global memory after a flush.
+// Output bytes are stored straight to the slot; a block's commit-time output
+// is held in registers and stored at the start of the NEXT block, after that
+// block's input waits (see held0): the waits then never cover young stores (a
+// wave's loads and stores share one counter, so a wait for a load issued
+// before a burst of stores would wait for the stores too).  The table is the
+// wave's only LDS.
 __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u32 n, u8* obase, u8* op_lim,
-                             u16* table, u32 ht, u8* pscr, u8* stg, u32 lane) {
+                             u16* table, u32 ht, u32 lane) {
   const int shift = 32 - (31 - __builtin_clz(ht));
 #ifdef FSG_STAMPS
   u64 st_[16] = {};
@@ -182,23 +149,11 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
   for (u32 i = 8 * lane; i < ht; i += 512) *reinterpret_cast<u32x4*>(table + i) = u32x4{0, 0, 0, 0};
   lds_fence();
   const u32 cap = op_lim ? (u32)(op_lim - obase) : 0xffffffffu;
-  u32 opos = 0, flushed = 0;
+  u32 opos = 0;
   auto room = [&](u32 bytes) -> bool { return cap == 0xffffffffu || opos + bytes + 16 <= cap; };
-  auto flush_to = [&](u32 upto) {
-#if FSG_WENC_DIRECT
-    flushed = upto;
-    return;
-#endif
-    lds_fence();
-    for (u32 b0 = flushed; b0 < upto; b0 += 64) {
-      const u32 i = b0 + lane;
-      if (i < upto) obase[i] = stg[i & 511];
-    }
-    flushed = upto;
-  };
   // nb (1..5) tag bytes, one lane per byte
   auto put_tag = [&](u64 tag, u32 nb) {
-    if (lane < nb) OUTB(opos + lane) = (u8)(tag >> (8 * (lane & 7)));
+    if (lane < nb) obase[opos + lane] = (u8)(tag >> (8 * (lane & 7)));
     opos += nb;
   };
   // literal [s, e): tag, then the bytes from the lanes holding them (this
@@ -214,14 +169,13 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
     }
     if (s >= B || (prev_ok && s + 64 >= B)) {
       const u32 qc = B + lane;
-      if (qc >= s && qc < e) OUTB(opos + qc - s) = (u8)xw0c;
+      if (qc >= s && qc < e) obase[opos + qc - s] = (u8)xw0c;
       if (prev_ok) {
         const u32 qp = B - 64 + lane;
-        if (qp >= s && qp < e) OUTB(opos + qp - s) = (u8)xw0p;
+        if (qp >= s && qp < e) obase[opos + qp - s] = (u8)xw0p;
       }
       opos += len;
     } else {
-      flush_to(opos);
       u8* d = obase + opos;
       for (u32 k0 = 0; k0 < len; k0 += 1024) {  // 1 KiB per step, 16 bytes per lane
         const u32 k = k0 + 16 * lane;
@@ -237,7 +191,6 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
         }
       }
       opos += len;
-      flushed = opos;
     }
   };
   // EmitCopy (snappy.cc:216-232): 64-byte pieces while len >= 68 (written
@@ -248,7 +201,6 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
     if (len >= 68) {
       const u32 n64 = (len - 68) / 64 + 1;
       const u32 t = copy_tag(offset, 64, &nb);  // 3 bytes
-      flush_to(opos);
       for (u32 i0 = 0; i0 < n64; i0 += 64) {
         const u32 i = i0 + lane;
         if (i < n64) {
@@ -259,7 +211,6 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
         }
       }
       opos += 3 * n64;
-      flushed = opos;
       len -= 64 * n64;
     }
     if (len > 64) {
@@ -281,7 +232,6 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
   // recorded ones first and take the paths above.
   u32 EQL = 0, ECM = 0, fEQL = 0, fECM = 0;
   u64 EvM = 0, FastEv = 0;
-#if FSG_WENC_DIRECT
   // A block's commit-time output (<= 128 bytes: one byte per lane in two
   // registers) is held until the next block has waited for its input and
   // issued its loads, then stored by two unconditional buffer stores (lanes
@@ -299,7 +249,6 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
     __builtin_amdgcn_raw_buffer_store_b8((u8)held1, orsrc, (int)o1, 0, 0);
     held_n = 0;
   };
-#endif
   auto emit_pending = [&](u32 B, u32 xw0c, u32 xw0p, bool hold = false) -> bool {
     if (!EvM) return true;
     const bool fe = (FastEv >> lane) & 1ull;
@@ -334,21 +283,17 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       if (r < tle) byte = ltv >> (8 * r);
       else if (r < tle + le) byte = x < 64 ? bp : bc;
       else byte = ctv >> (8 * ((r - tle - le) & 3));
-#if FSG_WENC_DIRECT
       if (hold && total <= 128) {
         if (j0 == 0) held0 = byte;
         else held1 = byte;
         continue;
       }
-#endif
-      if (j < total) OUTB(opos + j) = (u8)byte;
+      if (j < total) obase[opos + j] = (u8)byte;
     }
-#if FSG_WENC_DIRECT
     if (hold && total <= 128) {
       held_n = total;
       held_at = opos;
     }
-#endif
     opos += total;
     EvM = 0;
     FastEv = 0;
@@ -365,13 +310,9 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
     u32 curB = 0xffffffffu;  // base of the block whose input is in xw
     W5 xw{}, xw1{}, xwp{};
     Raw20 xr2{};  // input of block curB + 128, in flight
-#if FSG_WENC_AHEAD2
-    Raw20 xr3{};  // and of block curB + 192 (input loads two blocks ahead)
-#endif
     u32 Tn = 0;
     Raw20 cbn{};
     bool spec = false, prev_ok = false;
-    u32 pend_end = 0;  // output of the blocks before the current one ends here
     u32 guard = 0;
     for (;;) {
       if (++guard > n / 16 + 64) break;  // cannot happen: every block advances the parse
@@ -381,29 +322,17 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       if (curB != 0xffffffffu && B == curB + 64) {
         xwp = xw;
         xw = xw1;
-        xw1 = shifted20(xr2);  // issued a block ago (two with FSG_WENC_AHEAD2)
+        xw1 = shifted20(xr2);  // issued a block ago
         prev_ok = true;
-#if FSG_WENC_AHEAD2
-        xr2 = xr3;
-        xr3 = raw20(fr, fal + B + 192 + lane);
-#endif
       } else {
         const Raw20 r0 = raw20(fr, fal + B + lane), r1 = raw20(fr, fal + B + 64 + lane);
-#if FSG_WENC_AHEAD2
-        xr2 = raw20(fr, fal + B + 128 + lane);
-        xr3 = raw20(fr, fal + B + 192 + lane);
-#endif
         xw = shifted20(r0);
         xw1 = shifted20(r1);
         spec = false;
         prev_ok = false;
       }
-#if !FSG_WENC_AHEAD2
       xr2 = raw20(fr, fal + B + 128 + lane);
-#endif
       curB = B;
-      // the previous blocks' output, now that the waits above are behind us
-      flush_to(pend_end);
       STAMP(0);
       // a copy ending at this block's first position: its ip-1 insert was
       // committed by the previous block if that block was processed
@@ -427,13 +356,11 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       // slots and the first pred round go out together: one wait)
       const u32 T = table[h];
       const u32 Tn_next = table[h1];
-#if FSG_WENC_DIRECT
       lds_fence();
       table[h] = (u16)(B + lane);
       lds_fence();
       const u32 rb0 = table[h];
       lds_fence();
-#endif
       W5 cb;
       {
         // the speculative loads are right unless the previous block changed the slot
@@ -464,12 +391,9 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       Tn = Tn_next;
       cbn = raw20(fr, fal + Tn);
       spec = true;
-#if FSG_WENC_DIRECT
       store_held();  // the previous block's output (see held0)
-#endif
       STAMP(1);
       // ---- pred rounds (the table slots are restored by the commit)
-#if FSG_WENC_DIRECT
       // Every active lane writes its position into its slot (highest lane
       // wins) and reads it back; the winners leave and listen one more
       // round: what they read then is the winner of that round among their
@@ -500,34 +424,6 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
           active = active && !win;
         }
       }
-#else
-      pscr[lane] = (u8)kPredNone;
-      lds_fence();
-      {
-        bool active = true;
-        u32 lastwin = kPredNone;
-        for (int r = 0; r < 3; ++r) {
-          if (!__ballot(active)) break;
-          if (active) table[h] = (u16)(B + lane);
-          lds_fence();
-          const u32 rb = active ? (u32)table[h] : 0u;
-          lds_fence();
-          const bool win = active && rb == B + lane;
-          if (win && lastwin != kPredNone) pscr[lastwin] = (u8)lane;
-          lds_fence();
-          if (active && !win) lastwin = rb - B;
-          active = active && !win;
-        }
-        if (__ballot(active)) {
-          if (active) {
-            pscr[lane] = (u8)kPredUnknown;
-            if (lastwin != kPredNone) pscr[lastwin] = (u8)kPredUnknown;
-          }
-          lds_fence();
-        }
-      }
-      const u32 p1 = pscr[lane];
-#endif
       // (ds_bpermute reads 0 from a lane outside EXEC, so every permute runs
       // on all lanes and the selects come after)
       const u32 t2 = bperm(p1, p1 & 63);
@@ -576,7 +472,6 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
         return scan(j, Ims);
       };
 
-#if FSG_WENC_FAST == 2
       // ---- fast events, precomputed per lane k: the event a post-copy
       // arrival at B + k makes under the fast rules (snappy.cc:428-438 and
       // the stride-1 probes of :377-397): the probe at B + k by a lane with
@@ -614,54 +509,13 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
         fECM = (fpk & 0xffffu) | (fml << 16);
         FastM = __ballot(((Stat >> k) & 1ull) && (hit || miss_ok) && !lng);
       }
-#if FSG_WENC_CHAIN
-      // The walk below, for every arrival lane at once: lane k's chain is k,
-      // then its successor's lane while that lane is fast and its position
-      // lies below min(lim, B + 64).  Pointer doubling over the successor
-      // lanes: after round r, cm = the chain's first 2^r lanes, ci = their
-      // inserts, cn = where they leave.  A fast event advances >= 4
-      // positions (a 4-byte match), so a chain has <= 16 lanes: 4 rounds.
-      u32 cmlo, cmhi, cilo, cihi, cn;
-      {
-        const u32 stop = lim < B + 64 ? lim : B + 64;
-        const u32 nl = fsucc - B;
-        u32 J = (((FastM >> lane) & 1ull) && fsucc < stop && ((FastM >> (nl & 63)) & 1ull)) ? nl : 64u;
-        cmlo = lane < 32 ? 1u << lane : 0u;
-        cmhi = lane < 32 ? 0u : 1u << (lane - 32);
-        cilo = filo;
-        cihi = fihi;
-        cn = fsucc;
-        for (int r = 0; r < 4; ++r) {
-          if (!__ballot(J < 64)) break;
-          const u32 src = J < 64 ? J : lane;
-          const u32 jj = bperm(J, src), ml = bperm(cmlo, src), mh = bperm(cmhi, src);
-          const u32 il = bperm(cilo, src), ih = bperm(cihi, src), nj = bperm(cn, src);
-          if (J < 64) {
-            cmlo |= ml;
-            cmhi |= mh;
-            cilo |= il;
-            cihi |= ih;
-            cn = nj;
-            J = jj;
-          }
-        }
-      }
-#endif
       STAMP(12);
-#endif
       bool done = false, leave = false;
       for (u32 ev = 0; !done && !leave && ev < 200; ++ev) {
-#if FSG_WENC_FAST == 2
         // ---- fast events (see the per-lane precomputation above): a walk
         // over the lanes' successors while the arrival lane's event is fast,
         // up to the first arrival past the block or the input limit
         if (post && ((FastM >> (ip - B)) & 1ull)) {
-#if FSG_WENC_CHAIN
-          const u32 k0 = ip - B;
-          const u32 nip = rl(cn, k0);
-          const u64 evs = ((u64)rl(cmhi, k0) << 32) | (u64)rl(cmlo, k0);
-          const u64 iadd = ((u64)rl(cihi, k0) << 32) | (u64)rl(cilo, k0);
-#else
           const u32 stop = lim < B + 64 ? lim : B + 64;
           u32 k0 = ip - B, nip;
           u64 evs = 0, iadd = 0;
@@ -673,7 +527,6 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
             k0 = nip - B;
             if (!((FastM >> k0) & 1ull)) break;
           }
-#endif
           I |= iadd;
           EvM |= evs;
           FastEv |= evs;
@@ -685,59 +538,6 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
           STAMP(13);
         }
         if (done || leave || ev >= 200) break;
-#elif FSG_WENC_FAST
-        // ---- fast events: the common case of text, taken without the
-        // general path's machinery (ISA: ~25 scalar instructions and two
-        // readlanes per event instead of ~70 and a branch tree).  From the
-        // post-copy state: the probe at ip (snappy.cc:428-438) by a lane with
-        // no in-block predecessor; if it misses, the stride-1 probes of the
-        // literal search (skip 32..63, snappy.cc:377-397) up to their first
-        // T-match, with no predecessor lane among the probes before it; a
-        // match shorter than the 20 compared bytes; literal bytes in
-        // registers.  Any other case leaves the state untouched and falls
-        // through to the general event below, which decides it exactly.
-        while (post && ev < 200) {
-          const u32 k0 = ip - B;  // < 64: the block holds ip (else leave)
-          if (!((Stat >> k0) & 1ull)) break;
-          u32 fpk = rl(packT, k0);
-          u64 nI = I | (1ull << k0);
-          u32 fq = ip;
-          if (!(fpk >> 31)) {
-            const u32 a = k0 + 1;  // the search starts at ip + 1 with skip 32
-            if (a >= 64) break;
-            const u32 c = 64 - a < 32 ? 64 - a : 32u;
-            const u32 fp = ip + 1;
-            if ((lim >= fp ? lim - fp : 0u) < c) break;
-            const u64 S = ((1ull << c) - 1) << a;
-            const u64 Mst = S & Stat & MTb;
-            if (!Mst) break;
-            const u32 ks = (u32)__builtin_ctzll(Mst);
-            const u64 below = (1ull << ks) - 1;
-            if (S & ~Stat & below) break;
-            fpk = rl(packT, ks);
-            fq = B + ks;
-            nI |= S & ((below << 1) | 1ull);
-          }
-          u32 fml = (fpk >> 16) & 31u;
-          if (fml >= 20 && fq + 20 < n) break;
-          if (fml > n - fq) fml = n - fq;
-          const u32 L = fq - next_emit;
-          if (!(L == 0 || next_emit >= B || (prev_ok && next_emit + 64 >= B))) break;
-          const bool mine = lane == k0;
-          EQL = mine ? fq | (L << 16) : EQL;
-          ECM = mine ? (fpk & 0xffffu) | (fml << 16) : ECM;
-          EvM |= 1ull << k0;
-          ++ev;
-          I = nI;
-          ip = fq + fml;
-          next_emit = ip;
-          WCOUNT(9);
-          if (ip >= lim) { done = true; break; }
-          if (ip - 1 < B + 64) I |= 1ull << (ip - 1 - B);
-          if (ip >= B + 64) { leave = true; break; }
-        }
-        if (done || leave || ev >= 200) break;
-#endif
         u32 q = 0, pk = 0;
         bool found = false;
         const u32 key = (post ? ip : p) - B;  // the event's lane (see EvM)
@@ -879,7 +679,6 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       if ((I >> lane) & 1ull) table[h] = (u16)(B + lane);
       lds_fence();
       if (!emit_pending(B, X, xwp.w[0], true)) return nullptr;
-      pend_end = opos;
       STAMP(5);
       WCOUNT(8);
       if (done) break;
@@ -888,15 +687,12 @@ __device__ u8* wave_fragment(__amdgpu_buffer_rsrc_t fr, u32 fal, const u8* fb, u
       if ((npos & ~63u) != B + 64) spec = false;
     }
   }
-#if FSG_WENC_DIRECT
   store_held();  // the last block's output
-#endif
   if (next_emit < n) {
     if (!room(n - next_emit + 5)) return nullptr;
     // remainder (snappy.cc:446-450): bytes from global memory
     emit_literal(next_emit, n, 0xffffffffu, 0u, false, 0u);
   }
-  flush_to(opos);
   STAMP(6);
 #ifdef FSG_STAMPS
   if (lane == 0)
@@ -928,13 +724,6 @@ __global__ __launch_bounds__(64) void encode_wave_kernel(
     u32* __restrict__ ctr, const u32* __restrict__ items, u32* __restrict__ sizes, u32 region_cap,
     u32 share_permille, u64 all_bytes) {
   extern __shared__ __attribute__((aligned(16))) u16 wtab[];
-#if FSG_WENC_DIRECT
-  u8* const pscr = nullptr;
-  u8* const stg = nullptr;
-#else
-  __shared__ u8 pscr[64];
-  __shared__ __attribute__((aligned(16))) u8 stg[512];
-#endif
   const u32 lane = threadIdx.x;
   const u32 quota = (u32)__builtin_amdgcn_readfirstlane((int)wave_quota(ctr, share_permille, all_bytes));
   (void)n_msgs;
@@ -977,7 +766,7 @@ __global__ __launch_bounds__(64) void encode_wave_kernel(
     const __amdgpu_buffer_rsrc_t fr =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<u8*>(fb - fal), (short)0, (int)((fal + n + 3) & ~3u), 0x00020000);
     const u32 ht = table_size_for(n);
-    u8* end = wave_fragment(fr, fal, fb, n, op, op_lim, wtab, ht, pscr, stg, lane);
+    u8* end = wave_fragment(fr, fal, fb, n, op, op_lim, wtab, ht, lane);
     if (lane == 0) {
       if (staged) {
         sizes[w] = end ? (u32)(end - region) : 0xffffffffu;
@@ -989,11 +778,5 @@ __global__ __launch_bounds__(64) void encode_wave_kernel(
   }
 }
 
-// LDS bytes of encode_wave_kernel's table for a batch whose largest fragment
-// is max_frag bytes.
-size_t encode_wave_lds_bytes(u32 max_frag) { return (size_t)table_size_for(max_frag) * sizeof(u16); }
-// Static LDS of encode_wave_kernel besides the table (the staging ring and
-// the pred scratch when FSG_WENC_DIRECT is off), for the launch's waves per CU.
-size_t encode_wave_static_lds_bytes() { return FSG_WENC_DIRECT ? 0 : 640; }
 
 }  // namespace fsg

@@ -24,9 +24,12 @@ Outputs (all data, no code):
                  per-message (input_fnv, compressed_len, compressed_fnv) of all
                  65,536 C2 and C3 bodies, and for CM's 1,048,576 bodies the
                  aggregate digests (fnv1a64 over the per-message fnv column,
-                 sums of lengths) plus the compressed-length column.
+                 sums of lengths) plus the compressed-length column; for C5's
+                 262,144 SnappyMessageProto bodies the per-message
+                 (compressed_len, compressed_fnv) columns and the input
+                 aggregate.
                  `python tests/golden/make_golden.py --full-only` regenerates
-                 just these.
+                 just these (`--c5-only`: just full_C5.npz).
 """
 from __future__ import annotations
 
@@ -74,6 +77,20 @@ def full_digests(ref, kind, sizes, chunk=8192, threads=8):
     return in_fnv, clen, cfnv
 
 
+def make_full_c5(ref):
+    """C5 at full size: 262,144 SnappyMessageProto bodies (bench.py's
+    c5-compress batch), every body's compressed (length, fnv)."""
+    n = 262144
+    sizes = fsg.mixed_sizes(n)
+    in_fnv, clen, cfnv = full_digests(ref, fsg.KIND_PROTO, sizes, chunk=32768)
+    b_total = int(sum(len(fsg.make_batch(fsg.KIND_PROTO, sizes[a:a + 32768], first_index=a).data)
+                      for a in range(0, n, 32768)))
+    np.savez_compressed(HERE / "full_C5.npz", compressed_len=clen, compressed_fnv=cfnv,
+                        aggregate=np.array([aggregate(in_fnv), aggregate(cfnv)], np.uint64),
+                        totals=np.array([b_total, int(clen.astype(np.uint64).sum())], np.uint64))
+    print("C5 full:", n, "bodies,", b_total, "bytes, ratio %.3f" % (b_total / clen.sum()))
+
+
 def make_full(ref):
     n = 65536
     for name, kind, size in (("C2", fsg.KIND_RANDOM, 4096), ("C3", fsg.KIND_TEXT, 65536)):
@@ -89,10 +106,14 @@ def make_full(ref):
                         totals=np.array([int(sizes.astype(np.uint64).sum()), int(clen.astype(np.uint64).sum())],
                                         np.uint64))
     print("CM full:", n, "bodies,", int(sizes.astype(np.uint64).sum()), "bytes")
+    make_full_c5(ref)
 
 
 def main():
     ref = Reference()
+    if "--c5-only" in sys.argv:
+        make_full_c5(ref)
+        return
     if "--full-only" in sys.argv:
         make_full(ref)
         return

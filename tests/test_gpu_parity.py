@@ -156,7 +156,7 @@ def test_randomized_against_oracle(gpu, oracle, encoder):
 
 
 @pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1"), (0, "1p"), (0, "1s0"),
-                                          (0, "1s1"), (0, "1s2"), (0, "1t1")])
+                                          (0, "1s1"), (0, "1s2")])
 def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, fsg_opts):
     """Mutated and truncated streams (64 B to 70 KB bodies).  fork "1" runs
     the path of batches over 128K messages: plan pass, the large messages'
@@ -165,10 +165,8 @@ def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, fsg_opts):
     ~150 messages (FSG_SMALL_PERSIST); "1sK" with FSG_SPLIT_WALK=K (0: the
     small bodies executed in message order; 1: walk and execution split by
     size on two streams; 2: one execution launch in walk order; default 3:
-    two execution launches by size); "1t1" with the tiny-body pass (bodies
-    under 512 compressed bytes one per lane, off by default)."""
+    two execution launches by size)."""
     fsg_opts(decode_fork=fork[0])
-    fsg_opts(tiny_pass=1 if fork == "1t1" else 0)
     fsg_opts(small_persist="5" if fork == "1p" else "1792")
     fsg_opts(split_walk=fork[2] if fork.startswith("1s") else "3")
     gpu.codec.select_kernels(variant, 0)
@@ -341,18 +339,17 @@ def test_pattern_copies_and_ring_jumps(gpu, oracle, variant):
         gpu.codec.select_kernels(0, 0)
 
 
-@pytest.mark.parametrize("tiny", [1, 0])
-def test_tiny_body_pass(gpu, oracle, tiny, fsg_opts):
-    """Bodies under 512 compressed bytes on the forked path go through the
-    tiny-body pass (snappy_decode_tiny.hip: one lane per body, output in LDS):
-    text of every small size, hand-built streams (patterns of every offset,
-    COPY_4, 4-byte literal lengths, literals over 64 bytes from global memory),
-    random single literals, runs whose output exceeds the pass's 768 bytes
-    (the serial fallback), the reference's negative vectors and mutated
-    bodies, trailing zero-length literals -- bytes and statuses against the
-    oracle.  tiny=0: the same batch through the lane walk + execution."""
-    fsg_opts(decode_fork=1, tiny_pass=tiny)
-    rng = np.random.default_rng(77 + tiny)
+def test_small_bodies_forked(gpu, oracle, fsg_opts):
+    """Bodies under 512 compressed bytes on the forked path (the lane walk in
+    size-class order + the small bodies' execution): text of every small
+    size, hand-built streams (patterns of every offset, COPY_4, 4-byte
+    literal lengths, literals over 64 bytes from global memory), random
+    single literals, runs with a large output, the reference's negative
+    vectors and mutated bodies, trailing zero-length literals -- bytes and
+    statuses against the oracle.  (Round 5's one-lane-per-body pass for
+    these, measured slower, was removed in round 6.)"""
+    fsg_opts(decode_fork=1)
+    rng = np.random.default_rng(77)
     comps = []
     for n in list(range(1, 200, 7)) + list(range(200, 800, 23)):
         comps.append(oracle.compress(fsg.make_batch(fsg.KIND_TEXT, [n], first_index=n).item(0)))

@@ -153,36 +153,44 @@ def _agg(col):
     return fsg.fnv1a64(np.ascontiguousarray(col, np.uint64).tobytes())
 
 
-@pytest.mark.parametrize("name", ["C2", "C3", "CM"])
+@pytest.mark.parametrize("name", ["C2", "C3", "CM", "C5"])
 def test_full_size_fixtures(oracle, name):
     """The full-size reference digests (tests/golden/full_*.npz, SURVEY §8(c)
     item 4) agree with the committed prefix digests, their aggregates with
     their columns, and the C restatement reproduces a strided sample of the
-    whole batch (every 2,048th message; CM every 32,768th)."""
+    whole batch (every 2,048th message; CM every 32,768th, C5 every 8,192nd)."""
     f = np.load(GOLDEN / f"full_{name}.npz")
     d = np.load(GOLDEN / f"digests_{name}.npz")
     k = len(d["compressed_len"])
     assert np.array_equal(f["compressed_len"][:k], d["compressed_len"])
     n = len(f["compressed_len"])
-    assert n == (1 << 20 if name == "CM" else 65536)
-    if name != "CM":
+    assert n == {"CM": 1 << 20, "C5": 262144}.get(name, 65536)
+    if name in ("C2", "C3"):
         assert np.array_equal(f["compressed_fnv"][:k], d["compressed_fnv"])
         assert np.array_equal(f["input_fnv"][:k], d["input_fnv"])
         assert int(f["aggregate"][0]) == _agg(f["input_fnv"]) and int(f["aggregate"][1]) == _agg(f["compressed_fnv"])
         sizes = np.full(n, 4096 if name == "C2" else 65536, np.uint32)
         step = 2048
+    elif name == "C5":
+        assert np.array_equal(f["compressed_fnv"][:k], d["compressed_fnv"])
+        assert int(f["aggregate"][1]) == _agg(f["compressed_fnv"])
+        assert int(f["totals"][1]) == int(f["compressed_len"].astype(np.uint64).sum())
+        sizes = fsg.mixed_sizes(n)
+        step = 8192
     else:
         sizes = fsg.mixed_sizes(n)
         assert int(f["totals"][0]) == int(sizes.astype(np.uint64).sum())
         assert int(f["totals"][1]) == int(f["compressed_len"].astype(np.uint64).sum())
         step = 32768
-    kind = {"C2": fsg.KIND_RANDOM, "C3": fsg.KIND_TEXT, "CM": fsg.KIND_MIXED}[name]
+    kind = {"C2": fsg.KIND_RANDOM, "C3": fsg.KIND_TEXT, "CM": fsg.KIND_MIXED, "C5": fsg.KIND_PROTO}[name]
     for i in range(7, n, step):
         x = fsg.make_batch(kind, sizes[i:i + 1], first_index=i).item(0)
         c = oracle.compress(x)
         assert len(c) == f["compressed_len"][i], i
         if name != "CM":
-            assert fsg.fnv1a64(c) == f["compressed_fnv"][i] and fsg.fnv1a64(x) == f["input_fnv"][i], i
+            assert fsg.fnv1a64(c) == f["compressed_fnv"][i], i
+        if name in ("C2", "C3"):
+            assert fsg.fnv1a64(x) == f["input_fnv"][i], i
 
 
 # ---- UncompressAsMuchAsPossible and RawUncompressToIOVec restated
