@@ -30,7 +30,6 @@ hipError_t launch_headers(const u8* in, const u64* in_off, const u32* in_len,
                           u32 n_msgs, u32* ulen, int lenient, hipStream_t stream);
 size_t encode_tables_workspace_bytes(u32 n_msgs, u32 max_in_len, u32* slots_out);
 size_t encode_plan_bytes(u32 n_msgs, u32 max_in_len);
-bool encode_all_on_wave(u32 n_msgs, u32 max_in_len);
 hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
                             u32 n_msgs, u32 max_in_len, u8* out, const u64* out_off,
                             u32* out_len, i32* status, void* ws, size_t ws_bytes,
@@ -44,9 +43,9 @@ hipError_t launch_gather_blocks(const u64* src, const u32* len, const u64* dst_o
 hipError_t launch_decode_partial(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u32 frag,
                                  u8* out, const u64* out_off, const u32* out_cap, u32* got, u64* produced,
                                  i32* status, hipStream_t stream);
-hipError_t launch_iov_scatter(const u8* stage, const u64* stage_off, const u32* out_len, u32 n_msgs,
-                              const u64* iov_base, const u64* iov_len, const u32* iov_first, i32* status,
-                              hipStream_t stream);
+hipError_t launch_iov_scatter(const u8* in, const u64* in_off, const u32* in_len, const u8* stage,
+                              const u64* stage_off, const u32* out_len, u32 n_msgs, const u64* iov_base,
+                              const u64* iov_len, const u32* iov_first, i32* status, hipStream_t stream);
 size_t lz4_compress_workspace_bytes(u32 n_msgs);
 hipError_t launch_lz4_encode(const u8* in, const u64* in_off, const u32* in_len, u32 n_msgs, u8* out,
                              const u64* out_off, u32* out_len, i32* status, void* ws, hipStream_t stream);
@@ -87,11 +86,13 @@ constexpr OptDesc kOptDesc[fsg::kOptCount] = {
     {"exec_big_blocks", "FSG_EXEC_BIG_BLOCKS", 512},
     {"exec_prio", "FSG_EXEC_PRIO", 1},
     {"exec_big_blocks_fork", "FSG_EXEC_BIG_BLOCKS_FORK", 1024},
+    {"split_index", "FSG_SPLIT_INDEX", 0},
     {"encode_wave_min", "FSG_ENCODE_WAVE_MIN", 16384},
     {"encode_wave_share", "FSG_ENCODE_WAVE_SHARE", 500},
     {"encode_wave_all_mb", "FSG_ENCODE_WAVE_ALL_MB", 640},
     {"encode_lanes", "FSG_ENCODE_LANES", 0},
     {"encode_wave_per_cu", "FSG_ENCODE_WAVE_PER_CU", 0},
+    {"encode_wave_wg", "FSG_ENCODE_WAVE_WG", 1},
     {"lz4_big_min", "FSG_L4_BIG_MIN", -1},
 };
 std::atomic<int64_t> g_opt[fsg::kOptCount];
@@ -254,23 +255,11 @@ int fsg_compress_batch(const uint8_t* d_in, const uint64_t* d_in_off,
   const size_t need = fsg::encode_tables_workspace_bytes(n_msgs, max_in_len, &slots);
   if ((forced == 0 || forced == 3) && d_workspace && workspace_bytes >= need) {
     const fsg::u32 cap = max_in_len == 0 || max_in_len > fsg::kBlockSize ? fsg::kBlockSize : max_in_len;
-    // Lanes in flight.  Beside the wave encoder (a batch with units long
-    // enough for it), 3/4 of the messages, at most 131,072: the lanes' waves
-    // share the SIMDs with the wave encoder's lone waves, whose serial chains
-    // set the batch's time, and fewer lanes keep their tables and recent
-    // input cache-resident, each encoding more messages.  Measured (A/B, one
-    // box): C5 27.0 -> 18.8 ms (131,072 of 262,144; 98,304: 20.8, 196,608:
-    // 22.4), C3 92.3 -> 85.4 ms (49,152 of 65,536; 32,768: 85.3).  Option
-    // encode_lanes overrides (0 = this rule).
+    // Lanes in flight: option encode_lanes caps them; otherwise
+    // launch_encode_v3 caps them beside the wave encoder once it knows the
+    // wave encoder runs.
     const unsigned lanes_cap = (unsigned)fsg::opt(fsg::kOptEncodeLanes);
-    const fsg::u32 wmin = encode_wave_min();
-    if (lanes_cap) {
-      if (lanes_cap < slots) slots = (lanes_cap + 63) / 64 * 64;
-    } else if (wmin && n_msgs > 64 && (max_in_len >= wmin || fsg::encode_all_on_wave(n_msgs, max_in_len))) {
-      fsg::u32 beside = (fsg::u32)(((uint64_t)n_msgs * 3 / 4 + 255) / 256 * 256);
-      if (beside > 131072u) beside = 131072u;
-      if (beside < slots) slots = beside;
-    }
+    if (lanes_cap && lanes_cap < slots) slots = (lanes_cap + 63) / 64 * 64;
     return record(fsg::launch_encode_v3(d_in, d_in_off, d_in_len, n_msgs, max_in_len, d_out,
                                         d_out_off, d_out_len, d_status, d_workspace,
                                         workspace_bytes, slots, fsg::table_size_for(cap), need,
@@ -393,8 +382,8 @@ int fsg_decompress_batch_iovec(const uint8_t* d_in, const uint64_t* d_in_off, co
   const int r = decompress_impl(d_in, d_in_off, d_in_len, n_msgs, d_stage, d_stage_off, d_stage_cap, d_out_len,
                                 d_status, 0u, d_workspace, workspace_bytes, stream, nullptr);
   if (r != FSG_SUCCESS) return r;
-  return record(fsg::launch_iov_scatter(d_stage, d_stage_off, d_out_len, n_msgs, d_iov_base, d_iov_len, d_iov_first,
-                                        d_status, (hipStream_t)stream),
+  return record(fsg::launch_iov_scatter(d_in, d_in_off, d_in_len, d_stage, d_stage_off, d_out_len, n_msgs,
+                                        d_iov_base, d_iov_len, d_iov_first, d_status, (hipStream_t)stream),
                 "fsg_decompress_batch_iovec");
 }
 

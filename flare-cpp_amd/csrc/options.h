@@ -26,12 +26,14 @@ enum Opt : int {
   kOptExecBigBlocks,      // one-stream exec launch: large-message blocks
   kOptExecPrio,           // exec pass priority raise around round-A loads
   kOptExecBigBlocksFork,  // forked path: large-message exec blocks
+  kOptSplitIndex,         // one-stream lane walk of long bodies: two lanes per message (1) or one (0)
   // Snappy encode (capi.hip, snappy_encode_v3.hip)
   kOptEncodeWaveMin,      // long-unit threshold of the wave encoder (bytes; 0 = lanes only)
   kOptEncodeWaveShare,    // wave encoder's share of long units (permille)
   kOptEncodeWaveAllMb,    // all long units to the wave encoder below this many MiB
   kOptEncodeLanes,        // lanes in flight of the lane encoder (0 = all)
-  kOptEncodeWavePerCu,    // wave encoder blocks per CU (0 = as many as LDS holds)
+  kOptEncodeWavePerCu,    // wave encoder waves per CU (0 = as many as LDS holds)
+  kOptEncodeWaveWg,       // wave encoder waves per workgroup (1..5; their tables share the workgroup's LDS)
   // LZ4 two-pass decode (lz4_decode2.hip)
   kOptLz4BigMin,          // -1 automatic; blocks above this many bytes take the wave walk
   kOptCount

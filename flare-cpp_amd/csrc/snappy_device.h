@@ -85,6 +85,7 @@ __device__ __forceinline__ u32 hash_bytes(u32 bytes, int shift) {
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // ---- encode work units (encode_plan_kernel's long list)
+constexpr u32 kWaveEncMaxWaves = 5;      // waves per encode_wave_kernel workgroup (at most)
 constexpr u32 kWholeUnit = 0x80000000u;  // unit = a whole message (not a fragment of a split one)
 
 // Units [0, quota) of the long list go to the wave encoder, the rest to the

@@ -26,7 +26,10 @@
 //
 // Input bytes for hashing, for the winner's comparison and for short
 // literals come from an 80-byte per-lane window in LDS ([dword][lane]
-// layout), loaded with the candidates one batch ahead.
+// layout), loaded with the candidates one batch ahead.  (Round 6 measured
+// the window in registers, read by a barrel shift, so that the kernel needs
+// no LDS beside a five-table encode_wave_kernel workgroup: C3 even, C5
+// 18.8 -> 21.1 ms)
 //
 // Output bytes equal snappy::Compress(Source*, Sink*) (snappy.cc:875-954);
 // EmitLiteral / EmitCopy follow snappy.cc:156-232.
@@ -270,6 +273,13 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
         const u32 o = (u32)((int)pos - wbase);
         return abyte(wrd((o >> 2) + 1), wrd(o >> 2), o & 3);
       };
+      // 16 bytes at window offset o (o + 20 <= 80)
+      auto rd128 = [&](u32 o) -> u32x4 {
+        u32x4 v;
+#pragma unroll
+        for (u32 q = 0; q < 4; ++q) v[q] = abyte(wrd((o >> 2) + q + 1), wrd((o >> 2) + q), o & 3);
+        return v;
+      };
       auto in_win = [&](u32 pos, u32 len) -> bool {
         const int o = (int)pos - wbase;
         return o >= 0 && o + (int)len <= (int)(16 * kWinChunks);
@@ -399,10 +409,7 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
               u64 tag;
               const u32 tl = literal_tag(len, &tag);
               *op = (u8)tag;
-              const u32 o = (u32)((int)next_emit - wbase);
-              u32x4 v;
-#pragma unroll
-              for (u32 q = 0; q < 4; ++q) v[q] = abyte(wrd((o >> 2) + q + 1), wrd((o >> 2) + q), o & 3);
+              const u32x4 v = rd128((u32)((int)next_emit - wbase));
               __builtin_memcpy(op + tl, &v, 16);
               op += tl + len;
             } else {
@@ -414,9 +421,7 @@ __global__ __launch_bounds__(64) void encode_pipe_kernel(
           {
             u32x4 pb;
             if (in_win(p, 20)) {
-              const u32 o = (u32)((int)p - wbase);
-#pragma unroll
-              for (u32 q = 0; q < 4; ++q) pb[q] = abyte(wrd((o >> 2) + q + 1), wrd((o >> 2) + q), o & 3);
+              pb = rd128((u32)((int)p - wbase));
             } else if (fpos + p + 16 <= total) {
               __builtin_memcpy(&pb, fb + p, 16);
             } else {  // last bytes of the message: load [p-1, p+15) and shift
@@ -604,7 +609,6 @@ constexpr u32 kAllWaveMax = FSG_ENC_ALL_WAVE_MAX;
 __host__ __device__ inline bool all_on_wave(u32 n_msgs, u32 max_in_len) {
   return max_in_len >= kInputMarginBytes && (n_msgs <= kSmallBatchEnc || max_in_len <= kAllWaveMax);
 }
-bool encode_all_on_wave(u32 n_msgs, u32 max_in_len) { return all_on_wave(n_msgs, max_in_len); }
 size_t encode_plan_bytes(u32 n_msgs, u32 max_in_len) {
   if (max_in_len < kWaveMinBound && !all_on_wave(n_msgs, max_in_len)) return 0;
   u64 per_msg = ((u64)max_in_len + kBlockSize - 1) >> kBlockLog;
@@ -617,7 +621,8 @@ __global__ void encode_wave_kernel(const u8* __restrict__ in, const u64* __restr
                                    const u32* __restrict__ in_len, u32 n_msgs, u8* out,
                                    const u64* __restrict__ out_off, u32* __restrict__ out_len,
                                    i32* __restrict__ status, u32* __restrict__ ctr, const u32* __restrict__ items,
-                                   u32* __restrict__ sizes, u32 region_cap, u32 share_permille, u64 all_bytes);
+                                   u32* __restrict__ sizes, u32 region_cap, u32 share_permille, u64 all_bytes,
+                                   u32 tab_stride);
 
 // Per-device side stream for the wave encoder (created on first use; nullptr:
 // the wave encoder runs on the caller's stream before the lanes).
@@ -677,6 +682,19 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
   } else {
     wave_min = 0;
   }
+  // Lanes in flight beside the wave encoder (decided here, once it is known
+  // to run): 3/4 of the messages, at most 131,072.  The lanes' waves share
+  // the SIMDs with the wave encoder's waves, whose serial chains set the
+  // batch's time, and fewer lanes keep their tables and recent input
+  // cache-resident, each encoding more messages.  Measured (A/B, one box): C5
+  // 27.0 -> 18.8 ms (131,072 of 262,144; 98,304: 20.8, 196,608: 22.4), C3
+  // 92.3 -> 85.4 ms (49,152 of 65,536; 32,768: 85.3).  Option encode_lanes
+  // (a cap applied by the caller) replaces this rule.
+  if (wave_min && n_msgs > 64 && opt(kOptEncodeLanes) == 0) {
+    u32 beside = (u32)(((u64)n_msgs * 3 / 4 + 255) / 256 * 256);
+    if (beside > 131072u) beside = 131072u;
+    if (beside < slots) slots = beside;
+  }
   // (options encode_wave_share / encode_wave_all_mb: the tests force the lane
   // share with encode_wave_all_mb 0)
   const i64 share_opt = opt(kOptEncodeWaveShare), all_opt = opt(kOptEncodeWaveAllMb);
@@ -692,8 +710,26 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
   std::unique_lock<std::mutex> lk;
   if (wave_min) {
     const u32 cap = max_in_len > kBlockSize ? kBlockSize : max_in_len;
-    const u32 lds = table_size_for(cap) * 2;
-    u32 per_cu = (160u * 1024u) / lds;
+    const u32 ht = table_size_for(cap), lds = ht * 2;
+    // Workgroups of wg waves, one table each in the workgroup's LDS.  LDS is
+    // allocated per workgroup in 1,280-byte granules out of 163,840 per CU
+    // (profiles/r5/wenc/lds_resident_probe.txt: one-wave workgroups of
+    // 31,744 B fit five per CU, of 32,256 B four), so five 32 KiB tables fit
+    // only as one five-wave workgroup.
+    constexpr u32 kCuLds = 160u * 1024u, kLdsGranule = 1280u;
+    // Waves per workgroup (option encode_wave_wg, 1..5; default 1).  Five
+    // 32 KiB tables fit per CU only as one five-wave workgroup, which takes
+    // the CU's whole LDS: C3 with every unit on the wave encoder 159 -> 132
+    // ms, but beside the lanes (whose 80-byte LDS windows then find no room)
+    // C3 gained <= 1% and C5 lost 12% with the lanes' windows moved to
+    // registers, and batches of short bodies alone lost 33-60% (DESIGN.md
+    // section 5, round 6).
+    const i64 wg_opt = opt(kOptEncodeWaveWg);
+    u32 wg = wg_opt >= 1 && wg_opt <= (i64)kWaveEncMaxWaves ? (u32)wg_opt : 1u;
+    while (wg > 1 && wg * lds > kCuLds) --wg;
+    const u32 alloc = (wg * lds + kLdsGranule - 1) / kLdsGranule * kLdsGranule;
+    u32 per_cu = (kCuLds / alloc) * wg;
+    if (per_cu > 32) per_cu = 32;  // waves per CU
     const i64 pc_opt = opt(kOptEncodeWavePerCu);
     if (pc_opt > 0 && (u64)pc_opt < per_cu) per_cu = (u32)pc_opt;
     u32 waves = 256u * (per_cu ? per_cu : 1u);
@@ -711,8 +747,9 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
       if ((e = hipStreamWaitEvent(side->stream, side->fork, 0)) != hipSuccess) return e;
       wstream = side->stream;
     }
-    encode_wave_kernel<<<waves, 64, lds, wstream>>>(in, in_off, in_len, n_msgs, out, out_off, out_len, status, ctr,
-                                                   items, sizes, region_cap, kShare, kAllBytes);
+    if (wg > waves) wg = waves;
+    encode_wave_kernel<<<(waves + wg - 1) / wg, 64 * wg, wg * lds, wstream>>>(
+        in, in_off, in_len, n_msgs, out, out_off, out_len, status, ctr, items, sizes, region_cap, kShare, kAllBytes, ht);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (side && (e = hipEventRecord(side->join, side->stream)) != hipSuccess) return e;
   }

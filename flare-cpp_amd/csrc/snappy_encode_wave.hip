@@ -718,13 +718,22 @@ extern "C" int fsg_debug_wstamps(unsigned long long* out, int reset) {
 // placement as encode_pipe_kernel: a split message's fragment k goes to
 // region k of its slot (sizes[] = its length, or ~0 on overflow), a whole
 // message to its slot behind the varint header.
-__global__ __launch_bounds__(64) void encode_wave_kernel(
+//
+// A workgroup holds blockDim.x / 64 waves, each with its own table of
+// tab_stride entries in the workgroup's LDS (wave w: entries [w tab_stride,
+// (w + 1) tab_stride)); the waves share nothing else.  Five waves of 32 KiB
+// tables fill the CU's 160 KiB as ONE allocation: five one-wave workgroups of
+// 32 KiB do not fit (profiles/r5/wenc/lds_resident_probe.txt: four resident),
+// and a single workgroup may declare all 163,840 bytes (MI355X_MICROARCH.md,
+// occupancy).
+__global__ __launch_bounds__(64 * kWaveEncMaxWaves) void encode_wave_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u32 n_msgs,
     u8* out, const u64* __restrict__ out_off, u32* __restrict__ out_len, i32* __restrict__ status,
     u32* __restrict__ ctr, const u32* __restrict__ items, u32* __restrict__ sizes, u32 region_cap,
-    u32 share_permille, u64 all_bytes) {
-  extern __shared__ __attribute__((aligned(16))) u16 wtab[];
-  const u32 lane = threadIdx.x;
+    u32 share_permille, u64 all_bytes, u32 tab_stride) {
+  extern __shared__ __attribute__((aligned(16))) u16 wtab_all[];
+  const u32 lane = threadIdx.x & 63;
+  u16* const wtab = wtab_all + (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * tab_stride;
   const u32 quota = (u32)__builtin_amdgcn_readfirstlane((int)wave_quota(ctr, share_permille, all_bytes));
   (void)n_msgs;
   for (;;) {

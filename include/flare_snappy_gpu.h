@@ -123,9 +123,9 @@ int fsg_set_split_region_cap(uint32_t bytes);
  *   decode_fork (-1 | 0 | 1), split_walk (0..3), split_class, exec_keep
  *   (bytes of history at a window slide, 512..2000, multiple of 16),
  *   chunked_huge, small_persist, small_batch, split_huge, walk_order,
- *   lean_walk, exec_big_blocks, exec_prio, exec_big_blocks_fork,
+ *   lean_walk, exec_big_blocks, exec_prio, exec_big_blocks_fork, split_index,
  *   encode_wave_min, encode_wave_share, encode_wave_all_mb,
- *   encode_lanes, encode_wave_per_cu, lz4_big_min.
+ *   encode_lanes, encode_wave_per_cu, encode_wave_wg, lz4_big_min.
  * Every value produces the same bytes and statuses.  Set between batches, not
  * while other threads launch.  FSG_ERR_INVALID_ARG for an unknown name.
  * fsg_default_option returns the built-in default (before the environment). */
@@ -255,8 +255,12 @@ int fsg_decompress_batch_partial(const uint8_t *d_in, const uint64_t *d_in_off,
  * SnappyIOVecWriter does.  d_out_len[i] = the header's length.  d_status[i]:
  * FSG_OK (the reference's true; the iovecs hold its bytes, bytes past the
  * length untouched), FSG_CORRUPT / FSG_BAD_HEADER / FSG_IOV_TOO_SMALL (its
- * false; the iovecs are left untouched, where the reference leaves a decoded
- * prefix), or FSG_SLOT_TOO_SMALL (staging sizing error). */
+ * false; the iovecs hold what the reference leaves in place: the output's
+ * prefix filling every iovec for FSG_IOV_TOO_SMALL, the decoded prefix, a
+ * literal cut by the end of input and the last fast append's 16-byte spill
+ * for FSG_CORRUPT -- a rejected stream is re-walked serially by one lane,
+ * O(output bytes); nothing for FSG_BAD_HEADER), or FSG_SLOT_TOO_SMALL
+ * (staging sizing error; the iovecs are untouched). */
 int fsg_decompress_batch_iovec(const uint8_t *d_in, const uint64_t *d_in_off,
                                const uint32_t *d_in_len, uint32_t n_msgs,
                                const uint64_t *d_iov_base, const uint64_t *d_iov_len,

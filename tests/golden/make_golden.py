@@ -20,6 +20,12 @@ Outputs (all data, no code):
                  length, strict-header verdict, validator verdict
   digests_*.npz  per-message (compressed_len, fnv1a64) for the first N
                  messages of the C2/C3/CM/C5 synthetic batches
+  partial_frag.json  UncompressAsMuchAsPossible (snappy.cc:1530-1535) at
+                 source pieces of 1, 3 and 7 bytes: long-literal tags (1-4
+                 length bytes) placed to straddle a piece boundary (RefillTag's
+                 stitching, :790-847), exact and short header lengths, cut and
+                 corrupted tails -- the reference's return value and the bytes
+                 its sink received (`--partial-only` regenerates it)
   full_*.npz     the BASELINE configs at FULL size:
                  per-message (input_fnv, compressed_len, compressed_fnv) of all
                  65,536 C2 and C3 bodies, and for CM's 1,048,576 bodies the
@@ -109,8 +115,80 @@ def make_full(ref):
     make_full_c5(ref)
 
 
+def _long_literal(data: bytes, nbytes: int) -> bytes:
+    """LITERAL tag with `nbytes` (1-4) little-endian length bytes."""
+    n = len(data) - 1
+    return bytes([(59 + nbytes) << 2]) + n.to_bytes(nbytes, "little") + data
+
+
+def _varint(v: int) -> bytes:
+    out = bytearray()
+    while v >= 128:
+        out.append((v & 127) | 128)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def make_partial_frag(ref):
+    """Streams whose long-literal tag straddles a source-piece boundary at
+    pieces of 1, 3 and 7 bytes, decoded by the reference's
+    UncompressAsMuchAsPossible."""
+    rng = random.Random(1234)
+    cases = []
+    for frag in (1, 3, 7):
+        for nbytes in (1, 2, 3, 4):
+            for before in range(1, 5):  # the tag starts `before` bytes ahead of a piece end
+                for kind in ("exact", "short", "cut", "badcopy", "overrun"):
+                    lit_len = rng.choice([61, 64, 100, 200, 256] if nbytes == 1 else [61, 64, 100, 300, 1000])
+                    data = bytes(rng.randrange(97, 123) for _ in range(lit_len))
+                    # a prefix literal that puts the long tag `before` bytes ahead of a piece end
+                    pre = b""
+                    for plen in range(1, 40):
+                        cand = _lit(bytes(rng.randrange(65, 91) for _ in range(plen)))
+                        hdr_len = len(_varint(plen + lit_len + 8))
+                        start = hdr_len + len(cand)
+                        if (start + before) % frag == 0 or frag == 1:
+                            pre = cand
+                            break
+                    body = pre + _long_literal(data, nbytes) + _copy(4, 8)
+                    ulen = (len(pre) - 1) + lit_len + 8
+                    if kind == "short":
+                        ulen -= rng.randrange(1, lit_len // 2)
+                    elif kind == "overrun":
+                        ulen = (len(pre) - 1) + rng.randrange(1, lit_len)
+                    elif kind == "cut":
+                        body = body[: len(pre) + 1 + nbytes + rng.randrange(0, lit_len)]
+                    elif kind == "badcopy":
+                        body = body[:-2] + _copy(4000, 8)
+                    comp = _varint(ulen) + body
+                    r, got = ref.uncompress_as_much(comp, ulen, frag)
+                    cases.append({"frag": frag, "nbytes": nbytes, "before": before, "kind": kind,
+                                  "hex": comp.hex(), "ulen": ulen, "ret": r, "got_len": len(got),
+                                  "got_fnv": "%016x" % fsg.fnv1a64(got)})
+    (HERE / "partial_frag.json").write_text(json.dumps(cases, indent=1) + "\n")
+    print(len(cases), "partial_frag cases")
+
+
+def _lit(b: bytes) -> bytes:
+    n = len(b) - 1
+    if n < 60:
+        return bytes([n << 2]) + b
+    k = (n.bit_length() + 7) // 8
+    return bytes([(59 + k) << 2]) + n.to_bytes(k, "little") + b
+
+
+def _copy(off: int, ln: int) -> bytes:
+    if 4 <= ln <= 11 and off < 2048:
+        return bytes([((off >> 8) << 5) | ((ln - 4) << 2) | 1, off & 0xFF])
+    return bytes([((ln - 1) << 2) | 2]) + off.to_bytes(2, "little")
+
+
 def main():
     ref = Reference()
+    if "--partial-only" in sys.argv:
+        make_partial_frag(ref)
+        return
     if "--c5-only" in sys.argv:
         make_full_c5(ref)
         return
@@ -184,6 +262,7 @@ def main():
                  compressed_len=clen, compressed_fnv=cfnv)
         print(name, len(b), "bodies, ratio %.3f" % (b.total / max(1, int(clen.sum()))))
     print(len(vectors), "positive vectors,", len(neg), "negative vectors")
+    make_partial_frag(ref)
     make_full(ref)
 
 

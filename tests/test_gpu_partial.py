@@ -9,9 +9,10 @@ ABI (csrc/snappy_decode_partial.hip):
   source piece sizes;
 * fsg_decompress_batch_iovec = RawUncompressToIOVec (snappy.cc:1122-1132):
   the verdict and the iovecs' bytes against the oracle, on mutated streams and
-  random iovec lists (empty, exact, short and roomy ones).  On the reference's
-  `false` the device leaves the iovecs untouched (the reference leaves a
-  decoded prefix there; include/flare_snappy_gpu.h documents it)."""
+  random iovec lists (empty, exact, short and roomy ones).  The iovecs' bytes
+  are compared after a `false` verdict too: the decoded prefix the reference
+  leaves in place, a literal cut by the end of input, the spill of its last
+  16-byte fast append (SnappyIOVecWriter, snappy.cc:963-1120)."""
 import json
 from pathlib import Path
 
@@ -93,6 +94,21 @@ def test_as_much_golden(codec):
         assert (s == fsg.FSG_OK) == bool(v["ok"]), v["name"]
         quirk += p != len(g)
     assert quirk > 0
+
+
+@pytest.mark.parametrize("frag", [1, 3, 7])
+def test_as_much_small_pieces_golden(codec, oracle, frag):
+    """The reference's own UncompressAsMuchAsPossible results at 1-, 3- and
+    7-byte source pieces, long-literal tags straddling a piece boundary
+    (tests/golden/partial_frag.json; snappy.cc:790-847)."""
+    cases = [v for v in json.loads((GOLDEN / "partial_frag.json").read_text()) if v["frag"] == frag]
+    comps = [bytes.fromhex(v["hex"]) for v in cases]
+    prod, got, st = _partial(codec, comps, [max(v["ulen"], 1) for v in cases], frag)
+    for i, v in enumerate(cases):
+        key = (v["nbytes"], v["before"], v["kind"])
+        assert prod[i] == v["ret"], key
+        assert len(got[i]) == v["got_len"] and "%016x" % fsg.fnv1a64(got[i]) == v["got_fnv"], key
+        assert (st[i] == fsg.FSG_OK) == bool(oracle.uncompress(comps[i], cap=1 << 19)[0]), key
 
 
 @pytest.mark.parametrize("frag,fork", [(0, 0), (7, 0), (8160, 0), (8160, 1)])
@@ -191,6 +207,7 @@ def test_iovec_fuzz_against_oracle(codec, oracle, fork, fsg_opts):
     st, bufs, guards, caps, ulens = _iovec(codec, comps, iov_lens)
     assert (np.asarray(guards) == POISON).all()  # nothing written between iovecs
     seen = {True: 0, False: 0}
+    too_small = prefix = 0
     for i, c in enumerate(comps):
         h, ulen = hdr[i]
         if h and ulen > caps[i]:
@@ -198,15 +215,17 @@ def test_iovec_fuzz_against_oracle(codec, oracle, fork, fsg_opts):
             continue
         ok, rbufs = oracle.uncompress_iovec(c, iov_lens[i], fill=POISON)
         assert (st[i] == fsg.FSG_OK) == ok, (i, st[i])
-        if ok:
-            assert bufs[i] == rbufs, i
-        else:
+        assert bufs[i] == rbufs, (i, ok, st[i])  # the bytes the reference leaves, after a `false` too
+        if not ok:
             assert st[i] in (fsg.FSG_CORRUPT, fsg.FSG_BAD_HEADER, fsg.FSG_IOV_TOO_SMALL), i
-            assert all(x == bytes([POISON]) * len(x) for x in bufs[i]), i  # left untouched
             if h and oracle.uncompress(c)[0]:
                 assert st[i] == fsg.FSG_IOV_TOO_SMALL, i
+                too_small += 1
+            elif any(x != bytes([POISON]) * len(x) for x in rbufs):
+                prefix += 1
         seen[ok] += 1
     assert seen[True] > 100 and seen[False] > 100
+    assert too_small > 20 and prefix > 100, (too_small, prefix)
 
 
 def test_iovec_large_valid_batch(codec, oracle):

@@ -207,6 +207,23 @@ def test_oracle_as_much_golden(oracle, v):
     assert "%016x" % fsg.fnv1a64(got) == v["partial_fnv"]
 
 
+def _partial_frag_cases():
+    return json.loads((GOLDEN / "partial_frag.json").read_text())
+
+
+def test_oracle_as_much_small_pieces_golden(oracle):
+    """Long-literal tags straddling 1-, 3- and 7-byte source pieces (RefillTag
+    stitching, snappy.cc:790-847), pinned to the reference's own results
+    (tests/golden/partial_frag.json, make_golden.py)."""
+    cases = _partial_frag_cases()
+    assert len(cases) >= 200
+    for v in cases:
+        r, got = oracle.uncompress_as_much(bytes.fromhex(v["hex"]), v["ulen"], frag=v["frag"])
+        key = (v["frag"], v["nbytes"], v["before"], v["kind"])
+        assert r == v["ret"] and len(got) == v["got_len"], key
+        assert "%016x" % fsg.fnv1a64(got) == v["got_fnv"], key
+
+
 def _mutants(oracle, rng, count):
     srcs = [fsg.make_batch(fsg.KIND_TEXT, [s], first_index=s).item(0) for s in (40, 900, 20000, 70000, 140000)]
     for _ in range(count):

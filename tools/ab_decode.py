@@ -68,7 +68,12 @@ def main():
     # specs sharing one library path share its option table: every turn
     # starts from the values found at load time, then applies its own
     touched = sorted({k for _, _, kv in runs for k in kv})
-    initial = {id(c.lib): {k: fsg.get_option(k, c.lib) for k in touched} for _, c, _ in runs}
+    def _known(lib, k):
+        try:
+            return fsg.get_option(k, lib)
+        except KeyError:  # an older library without this option
+            return None
+    initial = {id(c.lib): {k: v for k in touched if (v := _known(c.lib, k)) is not None} for _, c, _ in runs}
     for r in range(args.rounds):
         for spec, codec, kv in runs:
             for k, v in {**initial[id(codec.lib)], **kv}.items():

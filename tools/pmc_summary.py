@@ -30,6 +30,24 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
 
 FETCH_SCALE = {"exec_kernel": 2.0, "index_kernel": 2.0, "index_big_kernel": 2.0}
+# Where each scale comes from (round 6, tools/probes/fetch_probe.hip,
+# profiles/r6/fetch/): FETCH_SIZE counts L2 misses only (16-B sc1 loads over
+# an L2-resident 1 MiB: 0.25 B per load) and tallies every missed 128-B line
+# at 64 B, for the exec pass's far-load pattern as for streaming: 16-B sc1
+# loads at random byte offsets report 68.5 B per load from a 96 MiB
+# Infinity-Cache-resident buffer and 71.4 B per load from 2 GiB (64 B per
+# line touched, 7-12% of the loads spanning two lines); at x2 the 2 GiB
+# kernel moved 5.55 TB/s and random whole-line loads 5.2-5.3 TB/s, beside
+# 4.84 TB/s for the calibrated x2 of a coalesced stream -- at x1 a kernel
+# with a million threads in flight would reach half the HBM rate a stream
+# does.  So the exec pass's far loads take x2 like its input reads.
+FETCH_SCALE_SOURCE = {
+    "exec_kernel": "profiles/r6/fetch/fp_FETCH_SIZE.csv: far_rand<1>/<2> (16-B sc1 loads at random byte offsets, "
+                   "the far-load pattern) 68.5/71.4 B per load = 64 B per 128-B line; x2 as the coalesced "
+                   "stream16 (0.5 GiB reported for 1 GiB read)",
+    "index_kernel": "profiles/r6/fetch/fp_FETCH_SIZE.csv: stream16 (1 GiB coalesced 16-B reads -> 0.5 GiB reported)",
+    "index_big_kernel": "profiles/r6/fetch/fp_FETCH_SIZE.csv: stream16 (as index_kernel)",
+}
 
 OP_KERNELS = {
     "decompress": ("index_kernel", "index_plan_kernel", "walk_offsets_kernel", "walk_scatter_kernel",
@@ -74,6 +92,8 @@ def main():
         scale = FETCH_SCALE.get(k, 1.0)
         out["kernels"][k] = {"fetch_kb_per_op": round(fa, 1), "write_kb_per_op": round(wa, 1),
                              "fetch_scale": scale, "dispatches": len(f.get(k, []))}
+        if k in FETCH_SCALE_SOURCE:
+            out["kernels"][k]["fetch_scale_source"] = FETCH_SCALE_SOURCE[k]
         fetch_kb += fa * scale
         write_kb += wa
     import bench
