@@ -26,7 +26,6 @@ enum Opt : int {
   kOptExecBigBlocks,      // one-stream exec launch: large-message blocks
   kOptExecPrio,           // exec pass priority raise around round-A loads
   kOptExecBigBlocksFork,  // forked path: large-message exec blocks
-  kOptSplitIndex,         // one-stream lane walk of long bodies: two lanes per message (1) or one (0)
   // Snappy encode (capi.hip, snappy_encode_v3.hip)
   kOptEncodeWaveMin,      // long-unit threshold of the wave encoder (bytes; 0 = lanes only)
   kOptEncodeWaveShare,    // wave encoder's share of long units (permille)

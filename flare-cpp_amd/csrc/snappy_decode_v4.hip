@@ -62,15 +62,6 @@ constexpr int kIdxTagsOne = 32, kIdxTagsPlanned = 24;
 // zeroed by the launch (see the lane walk's group stores).
 // Rounds B with pattern chunks outside the common path (see exec5_message).
 constexpr u32 kRingChunks = 16;              // 16-byte chunks per lane (256 B)
-constexpr u32 kSplitMinBody = 4096;          // kSplit: bodies walked by two lanes (compressed bytes)
-#ifndef FSG_SPLIT_RING
-#define FSG_SPLIT_RING 8
-#endif
-#ifndef FSG_SPLIT_GAP
-#define FSG_SPLIT_GAP 128
-#endif
-constexpr u32 kSplitRing = FSG_SPLIT_RING;   // kSplit: input ring chunks per lane (8: two waves per SIMD fit)
-constexpr u32 kSplitGap = FSG_SPLIT_GAP;     // kSplit: X is the first 512-byte boundary this far past s
 constexpr u32 kAhead = 7;                    // chunks prefetched per iteration
 // Waves per pass-1 workgroup.  One: most resident waves for large batches
 // (CM 15.1 ms vs 17.9 with four).  Four (82 KB of LDS: one workgroup per CU,
@@ -322,25 +313,7 @@ __global__ __launch_bounds__(256) void walk_scatter_kernel(
 
 // kPlanned: index_plan_kernel ran first (statuses, bitmap bases and the
 // large-message list are in place; only kNeedLaneWalk messages are walked).
-//
-// kSplit (one-stream batches of long bodies, C3): two lanes per message, so
-// a batch has twice the waves -- the walk is bound by one wave's issue rate
-// (a lone wave issues a VALU every 4 cycles, MI355X_MICROARCH.md constants),
-// and one wave per SIMD leaves half of each SIMD's issue slots idle.  Lanes
-// 0-31 (A) walk 32 messages from their first tag; lanes 32-63 (B) walk the
-// same messages from the middle s of the compressed body AS IF a tag started
-// there (pass 1b's chunked walk does the same with waves, chunk_spec_kernel).
-// A walks up to X = the first 512-byte boundary at least 128 bytes past s
-// and pauses at its chain's first position >= X; B records bits, output
-// length and checks only for its tags from X on, and its chain's first
-// position >= X.  Snappy tag chains started at different bytes meet within
-// ~10 bytes on text: once they share a position they
-// are one chain.  So if B's position at X equals A's, B's bits (groups from
-// X / 128 on, stored by B) and its length and checks are the message's, and
-// A combines them; otherwise A walks on from its pause to the end itself,
-// overwriting B's groups (same wave, later stores).  The tag walk's checks
-// are the same either way; the execution pass does the offset checks.
-template <bool kPlanned, bool kLean = false, u32 kW = kIdxWaves, bool kSplit = false>
+template <bool kPlanned, bool kLean = false, u32 kW = kIdxWaves>
 __global__ __launch_bounds__(64 * kW)
 __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     const u8* __restrict__ in, const u64* __restrict__ in_off,
@@ -355,10 +328,8 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   // VGPRs, 12.3 KB of LDS): an 8-chunk input ring, 16 tags per iteration, 4
   // chunks prefetched, 2 bit groups (an iteration's tags lie within the 128
   // bytes the ring holds, so within 2 groups of 128 input bytes).
-  // (kSplit: the lean ring and iteration, so two waves per SIMD fit in LDS)
-  constexpr bool kSmallRing = kLean || (kSplit && kSplitRing == 8);
-  constexpr int kIdxTags = kSmallRing ? 16 : (kPlanned ? kIdxTagsPlanned : kIdxTagsOne);
-  constexpr u32 kRC = kSmallRing ? 8 : kRingChunks, kRD = kRC * 4, kAH = kSmallRing ? 4 : kAhead;
+  constexpr int kIdxTags = kLean ? 16 : (kPlanned ? kIdxTagsPlanned : kIdxTagsOne);
+  constexpr u32 kRC = kLean ? 8 : kRingChunks, kRD = kRC * 4, kAH = kLean ? 4 : kAhead;
   // Bit groups (4 words each) per lane.  The one-stream walk (C2, C3) stores
   // its groups four at a time (kSuper: 64 bytes of bitmap, 512 input bytes,
   // as four back-to-back 16-byte stores of one lane), so the L2 merges them
@@ -412,10 +383,7 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   __syncthreads();
   // planned with a walk order: lane g walks message walk_perm[g], the
   // messages grouped by size class so a wave's lanes finish together
-  // (kSplit: 32 messages per wave, lanes l and l + 32 on message 32 w + l)
-  const bool segB = kSplit && lane >= 32;
-  const u32 gid = kSplit ? ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 32 + (lane & 31)
-                         : blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 gid = blockIdx.x * blockDim.x + threadIdx.x;
   // (walk_part 1 / 2: only the walk order's positions below / from the
   // first one of class split_class -- the larger / the smaller bodies)
   const bool ordered = kPlanned && walk_perm;
@@ -435,7 +403,7 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   i32 status = kOk;
   if (!kPlanned) {
     __shared__ u32 blk_s[kW + 1];
-    status = index_prologue(ib, n_in, valid_msg && !segB, m, lane, n_msgs, flags, out_cap, out_len,
+    status = index_prologue(ib, n_in, valid_msg, m, lane, n_msgs, flags, out_cap, out_len,
                             bm_counter, bm_base_out, bitmap, bm_capacity_words, big_count, big_list,
                             big_threshold, &ip, &expected, &bm_base, kW > 1 ? blk_s : nullptr);
   } else if (valid_msg && status_out[m] == kNeedLaneWalk) {
@@ -445,30 +413,8 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     bm_base = bitmap ? bm_base_out[m] : 0u;
     status = -1;
   }
-  // kSplit: B takes A's header, status and bitmap; xstop = A's pause point X
-  // (0xffffffff: no pause), rec_lo = the first position B records (0 for A)
-  u32 xstop = 0xffffffffu, rec_lo = 0, x_cross = 0xffffffffu;
-  bool paused = false, halves = false;
-  if constexpr (kSplit) {
-    const u32 src = lane & 31;
-    const i32 st_a = __shfl(status, (int)src, 64);
-    const u32 hdr = (u32)__shfl((int)ip, (int)src, 64);
-    expected = (u32)__shfl((int)expected, (int)src, 64);
-    bm_base = (u32)__shfl((int)bm_base, (int)src, 64);
-    const u32 body = n_in > hdr ? n_in - hdr : 0u;
-    const u32 s = hdr + body / 2;
-    const u32 X = (s + kSplitGap + 511) & ~511u;
-    halves = st_a < 0 && body >= kSplitMinBody && X < n_in;
-    if (segB) {
-      status = halves ? -1 : kOk;
-      ip = s;
-      rec_lo = X;
-    } else if (halves) {
-      xstop = X;
-    }
-  }
   const bool walked = status < 0;  // (planned: the other lanes' statuses stand)
-  u32* bm = bitmap && (!segB || halves) ? bitmap + bm_base : nullptr;
+  u32* bm = bitmap ? bitmap + bm_base : nullptr;
 
   const u32 ibal = (u32)(reinterpret_cast<uintptr_t>(ib) & 15);
   const u8* abase = ib - ibal;
@@ -487,17 +433,15 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   // a message without walking the bitmap (bm_base = kSingleLiteral | source).
   u32 single_src = 0;
   if (status < 0) {
-    // (B: the chunks from its start)
-    const u32 cb = segB ? (ip + ibal) >> 4 : 0u;
     u32x4 c0[4];
 #pragma unroll
     for (u32 c = 0; c < 4; ++c) {
-      const u32 k = cb + c <= last_chunk ? cb + c : last_chunk;
+      const u32 k = c <= last_chunk ? c : last_chunk;
       c0[c] = *reinterpret_cast<const u32x4*>(abase + 16 * k);
     }
 #pragma unroll
-    for (u32 c = 0; c < 4; ++c) ring_write(cb + c, c0[c], cb + c <= last_chunk);
-    wend = iend = (last_chunk + 1 < cb + 4) ? last_chunk + 1 : cb + 4;
+    for (u32 c = 0; c < 4; ++c) ring_write(c, c0[c], c <= last_chunk);
+    wend = iend = (last_chunk + 1 < 4) ? last_chunk + 1 : 4;
     // tag byte at ip (header <= 5 bytes) and its <= 4 length bytes lie in the
     // first 32 bytes of the aligned chunks (ibal + 9 < 32)
     const u32 P = ip + ibal;
@@ -512,7 +456,7 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     const u32 val = ext & (0xffffffffu >> ((32 - 8 * nbl) & 31));
     const u32 len = nbl ? val + 1u : l0;
     const u64 end = (u64)ip + 1 + nbl + len;
-    if (!segB && (c & 3) == 0 && end == n_in && ip < n_in && len == expected) single_src = ip + 1 + nbl;
+    if ((c & 3) == 0 && end == n_in && ip < n_in && len == expected) single_src = ip + 1 + nbl;
   }
 
   u32 op = 0;
@@ -523,7 +467,7 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
   // long literal that leaves it ends the lane's iteration).
 #pragma unroll
   for (u32 q = 0; q < kBW; ++q) bmr[q * kWave + lane] = 0;
-  u32 fg = rec_lo >> 7;  // lowest group that may still hold unstored bits (B: from X on)
+  u32 fg = 0;  // lowest group that may still hold unstored bits
 
   u32x4 g[kAH];
 #pragma unroll
@@ -532,16 +476,14 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
 
   __builtin_amdgcn_s_waitcnt(0);
   bool more = __any(status < 0);
-  for (int phase = 0; phase < (kSplit ? 2 : 1); ++phase) {
   while (more) {
     // ---------- parse up to kIdxTags tags from the ring
     // a tag at ip is parsed this iteration iff ip < lim: still parsing, before
     // the end of input, and its 5 bytes are in the ring
     u32 lim = 0;
-    if (status < 0 && !paused) {
+    if (status < 0) {
       const u32 ring_end = 16 * wend >= 4 + ibal ? 16 * wend - 4 - ibal : 0u;
       lim = (wend > last_chunk || ring_end > n_in) ? n_in : ring_end;
-      lim = lim < xstop ? lim : xstop;  // A pauses at X
     }
     // Software-pipelined: tag j+1's ring read is issued (in program order)
     // before tag j's checks and its ds_or, so the LDS latency overlaps them;
@@ -590,26 +532,17 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
       // larger lpart (a huge or wrapping 4-byte literal length) shows in lmax.
       // The bit and length of such a tag land only in state that a corrupt
       // message never stores.
-      // (kSplit B: only its tags from X on are recorded; x_cross = its
-      // chain's first position >= X)
-      const bool rec = kSplit ? look && ip >= rec_lo : look;
-      if constexpr (kSplit) x_cross = look && ip < rec_lo && ip_next >= rec_lo ? ip_next : x_cross;
-      lmax = rec && lpart > lmax ? lpart : lmax;
-      atomicOr(&bmr[((ip >> 5) & (kBW - 1)) * kWave + lane], rec ? 1u << (ip & 31) : 0u);
-      op += rec ? len : 0u;
+      lmax = look && lpart > lmax ? lpart : lmax;
+      atomicOr(&bmr[((ip >> 5) & (kBW - 1)) * kWave + lane], look ? 1u << (ip & 31) : 0u);
+      op += look ? len : 0u;
       ip = ip_next;
     }
-    const bool walking = status < 0 && !paused;
-    if (walking && (ip > n_in || lmax > n_in)) status = kCorrupt;
+    if (status < 0 && (ip > n_in || lmax > n_in)) status = kCorrupt;
     // writer space (:1166, :1400), checked once per iteration: op only grows,
     // and one iteration cannot wrap it (accepted literals fit the input)
-    if (walking && (op > expected || op < op_it)) status = kCorrupt;
-    // kSplit A: past X it pauses (at the end of input too: B's groups from X
-    // on are then replaced only after B has stored them, in the second phase)
-    if (kSplit && walking && status < 0 && ip >= xstop) paused = true;
+    if (status < 0 && (op > expected || op < op_it)) status = kCorrupt;
     // end of input between tags (RefillTag eof): the result, snappy.cc:858-868
-    // (kSplit B: the end reached; A checks the length)
-    if (walking && !paused && status < 0 && ip == n_in) status = segB || op == expected ? kOk : kCorrupt;
+    if (status < 0 && ip == n_in) status = op == expected ? kOk : kCorrupt;
 
     // ---------- store the bit groups the walk has left
     // The bitmap is not zeroed by the launch: every group of a message the
@@ -619,11 +552,10 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
     // remaining groups up to the allocation (ceil(n_in / 128)).
     if (bm && !single_src) {
       const u32 ngroups = (((n_in + 31) >> 5) + 3) >> 2;
-      // (a paused A: everything below X, a multiple of 512 bytes)
-      const u32 cur0 = status < 0 ? (paused ? xstop >> 7 : ip >> 7) : (status == kOk ? ngroups : 0u);
+      const u32 cur0 = status < 0 ? ip >> 7 : (status == kOk ? ngroups : 0u);
       // super-group stores: while walking, only the whole super-groups below
       // the current one; once the walk is over, everything up to the end
-      const u32 cur = kSuper && status < 0 && !paused ? cur0 & ~3u : cur0;
+      const u32 cur = kSuper && status < 0 ? cur0 & ~3u : cur0;
       if constexpr (kSuper) {
         // fg is a multiple of 4 until the walk ends: the super-group at fg
         // is one half of the 8-slot ring; past fg + 4 only after a long
@@ -690,40 +622,9 @@ __attribute__((amdgpu_waves_per_eu(kLean ? 6 : 1))) void index_kernel(
       gk_w = base;
       gn_w = cnt;
     }
-    more = __any(status < 0 && !paused);
+    more = __any(status < 0);
   }
-  if constexpr (kSplit) {
-    if (phase == 0) {
-      // A takes B's results: where B's chain crossed X, B's verdict and its
-      // output length from X on
-      const u32 xb = (u32)__shfl((int)x_cross, (int)(lane + 32) & 63, 64);
-      const i32 sb = __shfl(status, (int)(lane + 32) & 63, 64);
-      const u32 ob = (u32)__shfl((int)op, (int)(lane + 32) & 63, 64);
-      if (!segB && paused) {
-        paused = false;
-        if (xb == ip && sb >= 0) {
-          // B's verdict and groups stand; A stores nothing more (its ring holds
-          // no bits from X on, and its later group stores would replace B's)
-          status = sb == kOk && (u64)op + ob == expected ? kOk : kCorrupt;
-          fg = 0xffffffffu;
-        } else {
-          // the chains did not meet by X: A walks on from its pause.  Its ring
-          // holds no bits (the pause stored and cleared them); the groups from
-          // X up to its super-group hold B's bits and no tag of A's (a long
-          // literal may have carried A past X): zeros, and A's stores resume
-          // at its super-group, inside its 8-group ring
-          xstop = 0xffffffffu;
-          const u32 g_ip = (ip >> 7) & ~3u;
-          if (bm && !single_src)
-            for (u32 gi = fg; gi < g_ip; ++gi) *reinterpret_cast<u32x4*>(bm + 4 * gi) = u32x4{0, 0, 0, 0};
-          fg = g_ip > fg ? g_ip : fg;
-        }
-      }
-      more = __any(status < 0);
-    }
-  }
-  }
-  const bool mine = valid_msg && !segB && (!kPlanned || walked);
+  const bool mine = valid_msg && (!kPlanned || walked);
   if (mine) status_out[m] = status;
   if (mine && bitmap && status == kOk && single_src) bm_base_out[m] = kSingleLiteral | single_src;
 }
@@ -2649,11 +2550,6 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     else if (est_total_in < 16384ull * n_msgs)
       index_kernel<false, false, kIdxWavesSerial><<<(n_msgs + 64 * kIdxWavesSerial - 1) / (64 * kIdxWavesSerial),
                                                     64 * kIdxWavesSerial, 0, stream>>>(
-          in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
-          cap_words, big_count, big_list, big_threshold, nullptr, nullptr);
-    else if (opt(kOptSplitIndex) != 0)
-      // two lanes per message (see index_kernel's kSplit)
-      index_kernel<false, false, 1, true><<<(n_msgs + 31) / 32, 64, 0, stream>>>(
           in, in_off, in_len, n_msgs, out_cap, out_len, status, flags, counter, bm_base, bitmap,
           cap_words, big_count, big_list, big_threshold, nullptr, nullptr);
     else
