@@ -24,7 +24,11 @@
 //     source is cut into `frag`-byte pieces, as the reference's Peek hands
 //     them out (a literal is appended piece by piece, which changes where a
 //     failing append stops); 0 = one piece.  Corrupt streams are the rare
-//     path, so the lane walks them byte by byte.
+//     path: one lane walks each, moving literals and copies 16 bytes at a
+//     time where the bytes allow it (copies whose source lies 16 or more
+//     bytes back, inside the current 64 KiB block), else byte by byte -- a
+//     rejected message of L output bytes costs O(L / 16) to O(L) serial
+//     steps of one lane.
 //   iovec: the decoder writes the caller's staging slot; iov_scatter_kernel,
 //     one wave per accepted message, copies it into the message's iovecs in
 //     order.  When they hold fewer bytes than the header length the
@@ -59,7 +63,9 @@ struct Scatter {
     if (at + n > cap) {
       overflow = true;
     } else {
-      for (u64 i = 0; i < n; ++i) o[at + i] = p[i];
+      u64 i = 0;
+      for (; i + 16 <= n; i += 16) copy16(o + at + i, p + i);  // 16 bytes at a time
+      for (; i < n; ++i) o[at + i] = p[i];
     }
     blk_used += n;
     if (at + n > hi) hi = at + n;
@@ -85,7 +91,15 @@ struct Scatter {
   __device__ bool append_from_self(u64 offset, u64 len) {
     const u64 cur = full + blk_used;
     if (offset - 1u >= cur || expected - cur < len) return false;
-    for (u64 i = 0; i < len && !overflow; ++i) {
+    u64 i = 0;
+    // inside the current block, with the source 16 or more bytes back, a
+    // 16-byte chunk reads only bytes already written: whole chunks
+    if (offset >= 16 && blk_used + len <= blk_len && cur + len <= cap) {
+      for (; i + 16 <= len; i += 16) copy16(o + cur + i, o + cur - offset + i);
+      blk_used += i;
+      if (cur + i > hi) hi = cur + i;
+    }
+    for (; i < len && !overflow; ++i) {
       const u8 c = o[cur - offset + i];
       append(&c, 1);
     }
