@@ -87,7 +87,7 @@ constexpr OptDesc kOptDesc[fsg::kOptCount] = {
     {"exec_prio", "FSG_EXEC_PRIO", 1},
     {"exec_big_blocks_fork", "FSG_EXEC_BIG_BLOCKS_FORK", 1024},
     {"encode_wave_min", "FSG_ENCODE_WAVE_MIN", 16384},
-    {"encode_wave_share", "FSG_ENCODE_WAVE_SHARE", 500},
+    {"encode_wave_share", "FSG_ENCODE_WAVE_SHARE", 475},
     {"encode_wave_all_mb", "FSG_ENCODE_WAVE_ALL_MB", 640},
     {"encode_lanes", "FSG_ENCODE_LANES", 0},
     {"encode_wave_per_cu", "FSG_ENCODE_WAVE_PER_CU", 0},

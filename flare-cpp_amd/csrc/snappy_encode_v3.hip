@@ -696,9 +696,12 @@ hipError_t launch_encode_v3(const u8* in, const u64* in_off, const u32* in_len,
     if (beside < slots) slots = beside;
   }
   // (options encode_wave_share / encode_wave_all_mb: the tests force the lane
-  // share with encode_wave_all_mb 0)
+  // share with encode_wave_all_mb 0).  The wave encoder's share of the long
+  // units' bytes above the all-on-wave bound, in permille: C3, A/B on one box
+  // (profiles/r6/enc/ab_c3_share_sweep*.log), 400 86.3-86.9 ms, 425 80.8-81.0,
+  // 450 80.4-80.6, 475 80.2-80.3, 500 82.4-82.6, 550 89.6-90.1.
   const i64 share_opt = opt(kOptEncodeWaveShare), all_opt = opt(kOptEncodeWaveAllMb);
-  const u32 kShare = share_opt >= 0 && share_opt <= 1000 ? (u32)share_opt : 500u;  // permille
+  const u32 kShare = share_opt >= 0 && share_opt <= 1000 ? (u32)share_opt : 475u;  // permille
   const u64 kAllBytes = (all_opt >= 0 && all_opt < (1 << 24) ? (u64)all_opt : 640ull) << 20;
   auto pipe = max_in_len > kBlockSize || max_in_len == 0
                   ? encode_pipe_kernel<FSG_V3_PROBES_SPLIT, FSG_V3_POST_PROBES_SPLIT>
