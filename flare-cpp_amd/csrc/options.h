@@ -26,6 +26,7 @@ enum Opt : int {
   kOptExecBigBlocks,      // one-stream exec launch: large-message blocks
   kOptExecPrio,           // exec pass priority raise around round-A loads
   kOptExecBigBlocksFork,  // forked path: large-message exec blocks
+  kOptExecPack,           // forked path: short bodies per packed execution batch (0 = a wave per body)
   // Snappy encode (capi.hip, snappy_encode_v3.hip)
   kOptEncodeWaveMin,      // long-unit threshold of the wave encoder (bytes; 0 = lanes only)
   kOptEncodeWaveShare,    // wave encoder's share of long units (permille)

@@ -111,7 +111,7 @@ __device__ u32x4 g_dummy_chunk[1];
 // Diagnostic build only (-DFSG_STAMPS): per-phase cycle totals of exec_kernel,
 // summed over waves, read back with fsg_debug_stamps.
 #ifdef FSG_STAMPS
-__device__ unsigned long long g_stamps[16];
+__device__ unsigned long long g_stamps[24];  // 0-7 exec5_message phases; 8-15 exec5_packed phases, 16 its set-up, 17-20 counts
 #define STAMP(k) do { const u64 t_ = __builtin_amdgcn_s_memtime(); st_[k] += t_ - t_last_; t_last_ = t_; } while (0)
 #else
 #define STAMP(k) do { } while (0)
@@ -2188,6 +2188,505 @@ __device__ __forceinline__ void exec5_message(
 #endif
 }
 
+// ===========================================================================
+// Pass 2, packed (the forked path's short bodies, walk part 2): several
+// bodies per wave, their tags in ONE stream of 64-tag groups.
+//
+// Run one wave per body, a short body spends most of its time in set-up and
+// dependent round trips (its sizes, then its bitmap words, then its tag
+// bytes, then its literal bytes) and in half-empty groups (CM: 1.0M bodies
+// under 4 KiB compressed, ~64 tags each).  Here a wave takes a batch of up to
+// 64 bodies of the walk order, one per lane, so their sizes load in one round
+// trip, and lays their outputs end to end in one VIRTUAL output space: body j
+// at V_j, congruent to its slot address modulo 16, so no 16-byte block holds
+// two bodies.  The tag ring is filled from the bodies' bitmaps one after
+// another; an entry carries its body (j << 24 | position, kFirstTag on a
+// body's first tag, whose output length then includes the gap up to V_j).
+// From there the walk is exec5_message's on virtual positions: a tag's input
+// and slot offsets come from its body's lane by ds_bpermute, far copies load
+// through one buffer over the output, and the window flush writes each
+// body's blocks to its own slot.
+// Pass 1 left every body here kOk with tag lengths summing to its length, so
+// a body's first tag lands at V_j exactly.  The check pass 2 adds (copy
+// offsets, snappy.cc:1200/:1410/:1466) marks a body kCorrupt and drops the bad
+// tag; no other body is touched.  Single-literal bodies are copied by the wave
+// first.  A batch whose offsets do not fit 32 bits hands its bodies to pass 3
+// (kNeedFallback).
+// ===========================================================================
+#ifndef FSG_PACK_GUARD_STATUS
+#define FSG_PACK_GUARD_STATUS kNeedFallback
+#endif
+namespace {
+constexpr u32 kFirstTag = 1u << 23;
+__device__ __forceinline__ u32 lane_bperm(u32 v, u32 src) {
+  return (u32)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+__device__ __forceinline__ u32 wave_max(u32 v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u32 o = (u32)__shfl_xor((int)v, d, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+}  // namespace
+
+__device__ __forceinline__ void exec5_packed(
+    const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u8* out,
+    const u64* __restrict__ out_off, const u32* __restrict__ out_len, i32* __restrict__ status,
+    const u32* __restrict__ bm_base, const u32* __restrict__ bitmap, const u32* __restrict__ perm, u32 first,
+    u32 count, u32* ring, const u32* tagtab, u8* sb, const u32x4* sel_tab, const u32x4* mtab, u32 lane,
+    u32 keep_hist) {
+#ifdef FSG_STAMPS
+  u64 st_[16] = {};
+  u64 t_last_ = __builtin_amdgcn_s_memtime();
+#define PCOUNT(k) (st_[k] += 1)
+#else
+#define PCOUNT(k) do { } while (0)
+#endif
+  // ---------- the batch: one body per lane
+  const bool have = lane < count;
+  const u32 m = have ? perm[first + lane] : 0u;
+  const i32 st = have ? status[m] : kCorrupt;
+  const u32 bmb_m = have ? bm_base[m] : 0u;
+  const u32 n_in = have ? in_len[m] : 0u;
+  const u32 E_m = have ? out_len[m] : 0u;
+  const u64 io = have ? in_off[m] : 0ull;
+  const u64 oo = have ? out_off[m] : 0ull;
+  const u32 ial = (u32)(reinterpret_cast<uintptr_t>(in) & 15), oal = (u32)(reinterpret_cast<uintptr_t>(out) & 15);
+  const bool ok = have && st == kOk;
+  // offsets from the 16-aligned buffer bases must fit 32 bits (with slack for
+  // the 20-byte tag loads past a body's end)
+  const bool wide = io + ial + n_in + 64 >= (1ull << 32) || oo + oal + E_m + 64 >= (1ull << 32);
+  if (__ballot(ok && wide)) {
+    if (ok) status[m] = kNeedFallback;
+    return;
+  }
+  const u32 ioff_m = (u32)io + ial, ooff = (u32)oo + oal;
+  const u8* const inb = in - ial;
+  u8* const outb = out - oal;
+  // one buffer over the batch's input and one over its slots, to the furthest
+  // body's last dword (the range check is per dword: a dword reaching past
+  // num_records reads 0 whole)
+  const u32 in_lim = (wave_max(ok ? ioff_m + n_in : 0u) + 3) & ~3u;
+  const u32 out_lim = (wave_max(ok ? ooff + E_m : 0u) + 3) & ~3u;
+  const __amdgpu_buffer_rsrc_t irsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<u8*>(inb), (short)0, (int)in_lim, 0x00020000);
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(outb, (short)0, (int)out_lim, 0x00020000);
+
+  // ---------- single-literal bodies: copied by the wave
+  const bool single = ok && (bmb_m & kSingleLiteral) && E_m > 0;
+  for (u64 S1 = __ballot(single); S1; S1 &= S1 - 1) {
+    const u32 j = (u32)__builtin_ctzll(S1);
+    const u32 src = readlane(ioff_m, j) + (readlane(bmb_m, j) & ~kSingleLiteral);
+    const u32 dst = readlane(ooff, j), L = readlane(E_m, j);
+    PCOUNT(13);
+    for (u32 k0 = 0; k0 < L; k0 += 4096) {
+      Raw16 x[4];
+#pragma unroll
+      for (u32 r = 0; r < 4; ++r) x[r] = raw_load16(irsrc, src + k0 + 1024 * r + lane * 16);
+#pragma unroll
+      for (u32 r = 0; r < 4; ++r) {
+        const u32 k = k0 + 1024 * r + lane * 16;
+        if (k < L) store_exact(outb + (dst + k), shifted16(x[r]), L - k < 16 ? L - k : 16u);
+      }
+    }
+  }
+
+  // ---------- the other bodies, compacted to lanes 0 .. np-1 in walk order
+  // (ds_permute: lane i sends its body to lane rank(i)), then laid out
+  const bool pk = ok && !(bmb_m & kSingleLiteral) && E_m > 0;
+  const u64 P = __ballot(pk);
+  if (!P) {
+#ifdef FSG_STAMPS
+    STAMP(8);
+    if (lane == 0)
+      for (int k = 0; k < 16; ++k) atomicAdd(&g_stamps[8 + k], (unsigned long long)st_[k]);
+#endif
+    return;
+  }
+  const u32 np = (u32)__builtin_popcountll(P);
+  const u32 rank = (u32)__builtin_popcountll(P & ((1ull << lane) - 1));
+  const u32 to = pk ? rank : np + lane - rank;  // a permutation of the lanes
+  auto compact = [&](u32 x) -> u32 { return (u32)__builtin_amdgcn_ds_permute((int)(to << 2), (int)x); };
+  const u32 ioff = compact(ioff_m), bmb = compact(bmb_m), bm_id = compact(m);
+  const u32 c_ooff = compact(ooff), c_E = compact(E_m), c_nin = compact(n_in);
+  const bool body = lane < np;
+  const u32 sz = body ? ((c_ooff & 15u) + c_E + 15u) & ~15u : 0u;
+  const u32 V = dpp_incl_scan(sz) - sz + (c_ooff & 15u);  // body start
+  const u32 VE = V + c_E;                                 // body end
+  // (ds_bpermute reads 0 from a lane outside EXEC: every lane permutes, the
+  // select comes after)
+  const u32 ve_prev = lane_bperm(VE, lane - 1);
+  const u32 gap = lane ? V - ve_prev : 0u;  // < 32: up to the body's start
+  const u32 oadj = c_ooff - V;             // slot offset = virtual position + oadj
+  // the bodies' bitmaps as one run of words: body j's at [Wb_j, Wb_j + nw_j)
+  const u32 nw = body ? (c_nin + 31) >> 5 : 0u;
+  const u32 w_incl = dpp_incl_scan(nw);
+  const u32 Wtot = readlane(w_incl, 63);
+  const u32 misc = gap | ((w_incl - nw) << 5);  // gap, Wb
+  PCOUNT(11);
+  STAMP(8);
+
+  u32 head = 0, tail = 0;
+  u32 op = readlane(V, 0);
+  const u32 op_end = readlane(VE, np - 1);
+  int sbase = (int)(op & ~15u);  // virtual position of sb[0]
+  u32 flushed = op;              // virtual [.., flushed) is in the slots
+  u32 fl_j = 0;                  // the first body the flush may still write
+  auto zero_from = [&](u32 from) {  // 1 KiB of zeros at a 16-aligned offset
+    const u32 i = from + 16 * lane;
+    if (i < kWindow + 32) *reinterpret_cast<u32x4*>(sb + i) = u32x4{0, 0, 0, 0};
+  };
+  zero_from(0);
+  u32 zero_end = 1024;
+  wave_lds_fence();
+  // The ring fill reads kFillWords words of the run at vw, across bodies: the
+  // lane's word w = vw + lane / 4 belongs to body fbody (the body holding vw,
+  // fcur, or one starting inside the window).  Its load is issued one fill
+  // ahead (bmw, with fst = the lane's body | its word index in the body << 8).
+  u32 vw = 0, fcur = 0;
+  u32 bmw = 0, fst = 0;
+  auto fill_load = [&]() {
+    const u32 w = vw + (lane >> 2);
+    u32 j = fcur, mine = fcur;
+    for (;;) {  // bodies starting inside the window (uniform)
+      const u32 jn = j + 1;
+      if (jn >= np) break;
+      const u32 wbn = readlane(misc, jn) >> 5;
+      if (wbn >= vw + kFillWords) break;
+      mine = w >= wbn ? jn : mine;
+      j = jn;
+    }
+    const u32 wb = lane_bperm(misc, mine) >> 5, bb = lane_bperm(bmb, mine);
+    fst = mine | ((w - wb) << 8);
+    bmw = w < Wtot ? bitmap[bb + (w - wb)] : 0u;
+    // the body holding the next window's first word
+    fcur = j + 1 < np && (readlane(misc, j + 1) >> 5) == vw + kFillWords ? j + 1 : j;
+  };
+  fill_load();
+  u32 pf_head = 0xffffffffu, pf_cnt = 0;
+  u32x4 pd = u32x4{0, 0, 0, 0};
+  u32 pd4 = 0;
+  auto prefetch = [&](u32 p, u32 iof) {
+    const u32 a = (p + iof) & ~3u;
+    pd = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
+    pd4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
+  };
+  // the window's completed bytes [flushed, fe) to their bodies' slots
+  auto flush_to = [&](u32 fe) {
+    if (fe <= flushed) return;
+    u32 j = fl_j;
+    while (j < np) {
+      const u32 bV = readlane(V, j), bE = readlane(VE, j), bo = readlane(oadj, j);
+      if (bE > flushed) {
+        const u32 lo_b = flushed > bV ? flushed : bV, hi_b = fe < bE ? fe : bE;
+        for (u32 blk = (lo_b & ~15u) + 16 * lane; blk < hi_b; blk += 1024) {
+          const u32 lo = blk < lo_b ? lo_b : blk;
+          const u32 hi = blk + 16 < hi_b ? blk + 16 : hi_b;
+          if (hi - lo == 16) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(sb + ((int)blk - sbase));
+            __builtin_memcpy(outb + (blk + bo), &v, 16);
+          } else {
+            store_exact(outb + (lo + bo), lds_read16(sb + ((int)lo - sbase)), hi - lo);
+          }
+        }
+        if (bE > fe) break;  // the body goes on past fe
+      }
+      ++j;
+    }
+    fl_j = j;
+    flushed = fe;
+  };
+
+  // every iteration fills, takes a long literal or takes >= 1 tag (>= 2
+  // input bytes): more iterations than input bytes mean a broken invariant,
+  // and the batch's bodies then go to pass 3 (serial, exact)
+  const u32 guard_max = wave_max(pk ? n_in : 0u) * 64 + 1024;
+  u32 guard = 0;
+  for (;;) {
+    if (++guard > guard_max) {
+      if (pk) status[m] = FSG_PACK_GUARD_STATUS;
+      return;
+    }
+    // ---------- refill the tag ring from the bodies' bitmaps, in order
+    if (tail - head < 2 * kMaxPieces && vw < Wtot) {
+      u32 bits = (bmw >> (8 * (lane & 3))) & 0xffu;
+      const u32 bitbase = (fst >> 8) * 32 + 8 * (lane & 3);
+      const u32 cnt = __builtin_popcount(bits);
+      const u32 incl = dpp_incl_scan(cnt);
+      u32 slot = tail + incl - cnt;
+      const u32 hi_bits = (fst & 0xffu) << 24;
+      // a body's first tag: the lowest bit of its first word's first byte
+      // (the header is at most 5 bytes)
+      u32 first = bitbase == 0 ? kFirstTag : 0u;
+      while (bits) {
+        ring[slot & (kTagRing - 1)] = hi_bits | (bitbase + __builtin_ctz(bits)) | first;
+        first = 0;
+        ++slot;
+        bits &= bits - 1;
+      }
+      tail += readlane(incl, 63);
+      vw += kFillWords;
+      fill_load();
+      wave_lds_fence();
+      STAMP(0);
+      continue;
+    }
+    const u32 avail = tail - head;
+    if (avail == 0) break;
+    const u32 take0 = avail < 64 ? avail : 64u;
+    const bool valid = lane < take0;
+    const u32 ent = ring[(head + lane) & (kTagRing - 1)];
+    const u32 tj = ent >> 24, pos = ent & (kFirstTag - 1);
+    const u32 t_ioff = lane_bperm(ioff, tj);
+    if (pf_head != head || pf_cnt < take0) prefetch(pos, t_ioff);
+
+    // ---------- decode one tag per lane (checked by pass 1)
+    const u32 s = (pos + t_ioff) & 3u;
+    const u32 c = __builtin_amdgcn_alignbyte(pd[1], pd[0], s) & 0xffu;
+    const u32 e = tagtab[c];
+    const bool q = s == 3;
+    const u32 w0 = q ? pd[1] : pd[0], w1 = q ? pd[2] : pd[1], w2 = q ? pd[3] : pd[2];
+    const u32 w3 = q ? pd4 : pd[3];
+    const u32 b = (s + 1) & 3u;
+    const u32x4 xr = u32x4{__builtin_amdgcn_alignbyte(w1, w0, b), __builtin_amdgcn_alignbyte(w2, w1, b),
+                           __builtin_amdgcn_alignbyte(w3, w2, b), __builtin_amdgcn_alignbyte(pd4, w3, b)};
+    const u32 val = xr[0] & (0xffffffffu >> (e & 31u));
+    const bool is_lit = e & 64u;
+    const u32 len = (e & 32u) ? val + 1u : (e >> 8) & 0x7fu;
+    const u32 off = val + (e >> 20);
+    const u32 nb = (e >> 16) & 7u;
+    const u32 lsrc = pos + 1 + nb;  // body-relative
+
+    const u64 bigm = __ballot(valid && is_lit && len > 64);
+    STAMP(1);
+    if (bigm & 1ull) {
+      // ---------- long literal: straight to the slot by the whole wave; the
+      // window restarts behind it (pass 1 checked its length)
+      const u32 L = readlane(len, 0), S = readlane(lsrc, 0), j0 = readlane(tj, 0);
+      if (readlane(ent, 0) & kFirstTag) op += readlane(misc, j0) & 31u;
+      const u32 iof = readlane(ioff, j0), oad = readlane(oadj, j0);
+      flush_to(op);
+      for (u32 k0 = 0; k0 < L; k0 += 4096) {
+        Raw16 x[4];
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) x[r] = raw_load16(irsrc, iof + S + k0 + 1024 * r + lane * 16);
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) {
+          const u32 k = k0 + 1024 * r + lane * 16;
+          if (k < L) store_exact(outb + (op + k + oad), shifted16(x[r]), L - k < 16 ? L - k : 16u);
+        }
+      }
+      op += L;
+      flushed = op;
+      sbase = (int)(op & ~15u) - 16;
+      zero_from(0);
+      zero_end = 1024;
+      wave_lds_fence();
+      if (lane < 2) {
+        const u32 lo = (u32)sbase + 16 * lane;
+        if (lo < op) {
+          const u32 cnt = op - lo < 16 ? op - lo : 16u;
+          store_exact(sb + 16 * lane, rsrc_load16(irsrc, iof + S + L - (op - lo)), cnt);
+        }
+      }
+      wave_lds_fence();
+      head += 1;
+      pf_head = 0xffffffffu;
+      if (head == tail) {  // the bitmap words under the literal hold no tag
+        const u32 wl = (readlane(misc, j0) >> 5) + ((S + L) >> 5);
+        if (wl > vw) {
+          vw = wl;
+          fcur = j0;
+          fill_load();
+        }
+      }
+      STAMP(7);
+      PCOUNT(10);
+      continue;
+    }
+    const u32 take = bigm ? (u32)__builtin_ctzll(bigm) : take0;
+    const bool v = lane < take;
+
+    // ---------- output positions (a body's first tag carries the gap to its
+    // start): <= kGroupBytes per group
+    const u32 t_misc = lane_bperm(misc, tj);
+    const u32 g = (ent & kFirstTag) ? t_misc & 31u : 0u;
+    const u32 lv = v ? len + g : 0u;
+    const u32 incl = dpp_incl_scan(lv);
+    const u32 t_op = op + incl - lv + g;
+    const bool fits = v && incl <= kGroupBytes && t_op < op_end;
+    const u32 k_tags = (u32)__builtin_popcountll(__ballot(fits));
+    const u32 tot_len = readlane(incl, k_tags - 1);
+    // the writer's checks (snappy.cc:1166, :1200, :1400, :1410, :1466) against
+    // the tag's body; a failing tag marks its body and writes nothing
+    const u32 t_V = lane_bperm(V, tj), t_VE = lane_bperm(VE, tj);
+    const bool bad = fits && (len > t_VE - t_op || (!is_lit && (off == 0 || off > t_op - t_V)));
+    const u32 t_m = lane_bperm(bm_id, tj);
+    if (__ballot(bad)) {
+      if (bad) status[t_m] = kCorrupt;
+    }
+    const bool run = fits && !bad;
+
+    // ---------- slide the window if this group would overrun it
+    if (op + tot_len - sbase > kWindow) {
+      const int nsb = (int)((op - keep_hist) & ~15u);
+      if ((int)flushed < nsb + 16) flush_to(op & ~15u);
+      wait_all_memory();
+      const u32 shift = (u32)(nsb - sbase), keep = (u32)((int)op - nsb);
+      for (u32 k = 0; k < keep; k += 1024) {
+        const u32 i = k + 16 * lane;
+        u32x4 x = u32x4{0, 0, 0, 0};
+        if (i < keep) x = *reinterpret_cast<const u32x4*>(sb + shift + i);
+        wave_lds_fence();
+        if (i < keep) *reinterpret_cast<u32x4*>(sb + i) = x;
+        wave_lds_fence();
+      }
+      sbase = nsb;
+      zero_end = (keep + 15) & ~15u;
+    }
+    auto prefetch_next_and_zero = [&]() {
+      {
+        const u32 nh = head + k_tags;
+        const u32 na = tail - nh;
+        const u32 ncnt = na < 64 ? na : 64u;
+        const u32 nent = ring[(nh + lane) & (kTagRing - 1)];
+        prefetch(nent & (kFirstTag - 1), lane_bperm(ioff, nent >> 24));
+        pf_head = nh;
+        pf_cnt = ncnt;
+      }
+      while (op + tot_len + 20 - sbase > zero_end) {
+        zero_from(zero_end);
+        zero_end += 1024;
+      }
+      wave_lds_fence();
+    };
+
+    STAMP(2);
+    // ---------- chunks (as exec5_message; far sources through the slots' buffer)
+    const u32 src = is_lit ? lsrc : t_op - off;
+    const u32 nch = (len + 15) >> 4;
+    const bool pat = !is_lit && off < 16 && off < len;
+    const u32 below = (u32)(sbase - (int)src);  // > 0 as int: far
+    const u32 kfar = (int)below > 0 ? ((below - 1) >> 4) + 1 : 0u;
+    const u32 kready = src + len <= op ? nch : (src < op ? (op - src) >> 4 : 0u);
+    const u32 klead = kfar > kready ? kfar : kready;
+    const u32 kc = pat ? 0u : (klead < nch ? klead : nch);
+    const u32 kf = run ? (is_lit ? nch : kc) : 0u;
+    const bool reg0 = is_lit && nb == 0;
+    const u32 t_oadj = lane_bperm(oadj, tj);
+    const u32 sh = is_lit ? (src + t_ioff) & 3u : 0u;
+    auto gload = [&](u32 k, u32x4& d, u32& d4) {
+      if (is_lit) {
+        const u32 a = (src + 16 * k + t_ioff) & ~3u;
+        d = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
+        d4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
+      } else if (k >= kfar) {
+        d = lds_read16(sb + ((int)(src + 16 * k) - sbase));
+      } else {
+        d = far_load(orsrc, src + 16 * k + t_oadj);
+      }
+    };
+    auto shf = [&](const u32x4& d, u32 d4, u32 t) {
+      return u32x4{__builtin_amdgcn_alignbyte(d[1], d[0], t), __builtin_amdgcn_alignbyte(d[2], d[1], t),
+                   __builtin_amdgcn_alignbyte(d[3], d[2], t), __builtin_amdgcn_alignbyte(d4, d[3], t)};
+    };
+    u32x4 a0 = xr, a1 = u32x4{0, 0, 0, 0};
+    u32 a0e = 0, a1e = 0;
+    if (kf > 0 && !reg0) gload(0, a0, a0e);
+    const u64 m1 = __ballot(kf > 1);
+    if (m1 && kf > 1) gload(1, a1, a1e);
+    prefetch_next_and_zero();
+    STAMP(3);
+    {
+      const u32 fe = op & ~15u;
+      if (fe >= flushed + 1024) flush_to(fe);
+    }
+    STAMP(4);
+    const u32 wa = (u32)((int)t_op - sbase);
+    if (kf > 0) or_store(sb, wa, shf(a0, a0e, reg0 ? 0u : sh), len < 16 ? len : 16u, mtab);
+    if (m1) {
+      if (kf > 1) or_store(sb, wa + 16, shf(a1, a1e, sh), len - 16 < 16 ? len - 16 : 16u, mtab);
+      if (__ballot(kf > 2)) {
+        if (kf > 2) gload(2, a0, a0e);
+        if (kf > 3) gload(3, a1, a1e);
+        if (kf > 2) or_store(sb, wa + 32, shf(a0, a0e, sh), len - 32 < 16 ? len - 32 : 16u, mtab);
+        if (kf > 3) or_store(sb, wa + 48, shf(a1, a1e, sh), len - 48, mtab);
+      }
+    }
+    wave_lds_fence();
+
+    STAMP(5);
+    // ---------- rounds B (as exec5_message)
+    u32 rem = (run && kf < nch) ? len - 16 * kf : 0u;
+    u32 cw = (u32)((int)t_op - sbase) + 16 * kf;
+    u32 sw = (u32)((int)src - sbase) + 16 * kf;
+    const u32 stp = pat ? pat_step(off) : 16u;
+    u32 n = rem < stp ? rem : stp;
+    bool pf = pat;
+    u32 ne = rem ? (pf ? cw : sw + n) : 0xffffffffu;
+    u64 pend = __ballot(rem > 0);
+    if (!__ballot(pat && rem > 0)) {
+      while (pend) {
+        const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
+        if (ne <= W) {
+          const u32x4 x = lds_read16(sb + sw);
+          const u32x4 o = lds_read16(sb + cw);
+          const u32x4 mk = mtab[n];
+          u32x4 y;
+          y[0] = (x[0] & mk[0]) | (o[0] & ~mk[0]);
+          y[1] = (x[1] & mk[1]) | (o[1] & ~mk[1]);
+          y[2] = (x[2] & mk[2]) | (o[2] & ~mk[2]);
+          y[3] = (x[3] & mk[3]) | (o[3] & ~mk[3]);
+          __builtin_memcpy(sb + cw, &y, 16);
+          rem -= n;
+          cw += n;
+          sw += n;
+          n = rem < 16u ? rem : 16u;
+          ne = rem ? sw + n : 0xffffffffu;
+        }
+        wave_lds_fence();
+        pend = __ballot(rem > 0);
+      }
+    }
+    while (pend) {
+      const u32 W = readlane(cw, (u32)__builtin_ctzll(pend));
+      if (ne <= W) {
+        u32x4 x = lds_read16(sb + sw);
+        if (pf) x = expand_pattern(x, off, sel_tab);
+        const u32x4 o = lds_read16(sb + cw);
+        const u32x4 mk = mtab[n];
+        u32x4 y;
+        y[0] = (x[0] & mk[0]) | (o[0] & ~mk[0]);
+        y[1] = (x[1] & mk[1]) | (o[1] & ~mk[1]);
+        y[2] = (x[2] & mk[2]) | (o[2] & ~mk[2]);
+        y[3] = (x[3] & mk[3]) | (o[3] & ~mk[3]);
+        __builtin_memcpy(sb + cw, &y, 16);
+        rem -= n;
+        cw += n;
+        sw = pat ? cw - stp : sw + n;
+        pf = false;
+        n = rem < stp ? rem : stp;
+        ne = rem ? sw + n : 0xffffffffu;
+      }
+      wave_lds_fence();
+      pend = __ballot(rem > 0);
+    }
+    op += tot_len;
+    head += k_tags;
+    STAMP(6);
+    PCOUNT(9);
+  }
+  flush_to(op);
+#ifdef FSG_STAMPS
+  STAMP(4);
+  if (lane == 0)
+    for (int k = 0; k < 16; ++k) atomicAdd(&g_stamps[8 + k], (unsigned long long)st_[k]);
+#endif
+  (void)op_end;
+}
+
 
 // 7 waves per SIMD by default (FSG_EXEC_WAVES; 72 VGPRs, 22.2 KB of LDS per
 // block with the 3 KiB window: C3 6.35 -> 6.20 ms against 6 waves with a
@@ -2300,11 +2799,51 @@ __global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_pe
   }
 }
 
+// The packed execution pass (exec5_packed) over walk part 2 (the bodies of
+// size class >= split_class): batches of `batch` consecutive walk positions
+// from a work counter.
+#ifndef FSG_PACK_WAVES
+#define FSG_PACK_WAVES 6
+#endif
+__global__ __launch_bounds__(kWavesPerBlock * 64) __attribute__((amdgpu_waves_per_eu(FSG_PACK_WAVES, FSG_PACK_WAVES))) void exec_packed_kernel(
+    const u8* __restrict__ in, const u64* __restrict__ in_off, const u32* __restrict__ in_len, u8* out,
+    const u64* __restrict__ out_off, const u32* __restrict__ out_len, i32* __restrict__ status,
+    const u32* __restrict__ bm_base, const u32* __restrict__ bitmap, const u32* __restrict__ walk_perm,
+    const u32* __restrict__ walk_hist, u32 split_class, u32* __restrict__ batch_next, u32 batch, u32 keep_hist) {
+  __shared__ __attribute__((aligned(16))) u8 wl_s[kWavesPerBlock][4 * kTagRing + kWindow + 32];
+  __shared__ u32x4 sel_tab[16];
+  __shared__ u32 tagtab[256];
+  __shared__ u32x4 mask_tab[17];
+  static_assert(kWavesPerBlock * 64 == 256, "one tag table entry per thread");
+  if (threadIdx.x < 64) init_pattern_table(sel_tab, threadIdx.x);
+  tagtab[threadIdx.x] = exec_tag_entry(threadIdx.x);
+  init_mask_table(mask_tab, threadIdx.x);
+  __syncthreads();
+  const u32 wv = (u32)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const u32 lane = threadIdx.x & 63;
+  u32* ring = reinterpret_cast<u32*>(wl_s[wv]);
+  u8* sb = wl_s[wv] + 4 * kTagRing;
+  const u32 n_walk = walk_hist[2 * kWalkClasses];
+  const u32 tcls = split_class >> 8;
+  const u32 lo = walk_hist[kWalkClasses + (split_class & 0xffu)];
+  const u32 hi = tcls ? walk_hist[kWalkClasses + tcls] : n_walk;
+  const u32 n = hi > lo ? hi - lo : 0u;
+  for (;;) {
+    const u32 got = atomicAdd(batch_next, lane == 0 ? 1u : 0u);
+    const u32 bi = (u32)__builtin_amdgcn_readfirstlane((int)got);
+    if ((u64)bi * batch >= n) break;
+    const u32 first = bi * batch;
+    const u32 cnt = n - first < batch ? n - first : batch;
+    exec5_packed(in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, walk_perm, lo + first, cnt,
+                 ring, tagtab, sb, sel_tab, mask_tab, lane, keep_hist);
+  }
+}
+
 #ifdef FSG_STAMPS
 extern "C" int fsg_debug_stamps(unsigned long long* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps));
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[24] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z));
   }
   return e == hipSuccess ? 0 : -1;
@@ -2356,12 +2895,13 @@ constexpr u32 kWsChunkSpecNext = 84;   //   work counters of its passes
 constexpr u32 kWsChunkFixNext = 88;
 constexpr u32 kWsChunkCheckNext = 92;
 constexpr u32 kWsChunkFinalNext = 100;
+constexpr u32 kWsPackNext = 104;      // packed execution: batch counter
 constexpr u32 kWsCounterBytes = 256;
 // the counters are distinct u32 slots inside the 256-byte header
 constexpr u32 kWsOffsets[] = {kWsBmCounter, kWsSet1BigNext, kWsSet1SegCount, kWsSet1WholeCount, kWsBigCount,
                               kWsHugeCount, kWsSet0BigNext, kWsSet0SegCount, kWsSet0ExecNext, kWsSet0WholeCount,
                               kWsSet1ExecNext, kWsChunkCount, kWsChunkSpecNext, kWsChunkFixNext,
-                              kWsChunkCheckNext, kWsChunkFinalNext};
+                              kWsChunkCheckNext, kWsChunkFinalNext, kWsPackNext};
 constexpr bool ws_offsets_ok() {
   for (u32 i = 0; i < sizeof(kWsOffsets) / sizeof(kWsOffsets[0]); ++i) {
     if (kWsOffsets[i] % 4 || kWsOffsets[i] + 4 > kWsCounterBytes) return false;
@@ -2690,6 +3230,23 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
         part ? walk_hist : nullptr, part, kSplitClass);
     return hipGetLastError();
   };
+  // The short bodies of walk part 2 packed several to a wave (exec5_packed):
+  // option exec_pack = bodies per batch (1..64; 0, the default = one wave per
+  // body, the small-message grid above).  Grid: the small-message grid's
+  // size.  Measured on CM (A/B on one box):
+  // 6.60-6.63 ms at 16/32/64 bodies per batch against 6.11-6.19 with one
+  // wave per body; the packed pass itself ran as long as the wave-per-body
+  // launch it replaces (2.97 vs 2.99 ms) and the side streams beside it
+  // slowed (pass 1b 3.88 -> 4.43 ms).
+  const i64 pack_opt = opt(kOptExecPack);
+  const u32 kPackBatch = pack_opt >= 1 && pack_opt <= 64 ? (u32)pack_opt : 0u;
+  auto launch_packed = [&](hipStream_t st) -> hipError_t {
+    const u32 grid = kSmallPersist && kSmallPersist < small_blocks ? kSmallPersist : small_blocks;
+    exec_packed_kernel<<<grid, kWavesPerBlock * 64, 0, st>>>(
+        in, in_off, in_len, out, out_off, out_len, status, bm_base, bitmap, walk_perm, walk_hist, kSplitClass,
+        reinterpret_cast<u32*>(w + kWsPackNext), kPackBatch, keep_hist);
+    return hipGetLastError();
+  };
   SideStream* side = fork ? side_stream() : nullptr;
   if (side) {
     // the plan pass lists the large messages; pass 1b starts on them while
@@ -2735,7 +3292,7 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
       if (kWalkOrder && split_mode == 2) {
         if ((e = launch_small(stream, 3u)) != hipSuccess) return e;
       } else if (kWalkOrder && split_mode == 3) {
-        if ((e = launch_small(stream, 2u)) != hipSuccess) return e;
+        if ((e = kPackBatch ? launch_packed(stream) : launch_small(stream, 2u)) != hipSuccess) return e;
         if ((e = launch_small(stream, 1u)) != hipSuccess) return e;
       } else {
         if ((e = launch_small(stream, 0u)) != hipSuccess) return e;

@@ -123,7 +123,7 @@ int fsg_set_split_region_cap(uint32_t bytes);
  *   decode_fork (-1 | 0 | 1), split_walk (0..3), split_class, exec_keep
  *   (bytes of history at a window slide, 512..2000, multiple of 16),
  *   chunked_huge, small_persist, small_batch, split_huge, walk_order,
- *   lean_walk, exec_big_blocks, exec_prio, exec_big_blocks_fork,
+ *   lean_walk, exec_big_blocks, exec_prio, exec_big_blocks_fork, exec_pack,
  *   encode_wave_min, encode_wave_share, encode_wave_all_mb,
  *   encode_lanes, encode_wave_per_cu, encode_wave_wg, lz4_big_min.
  * Every value produces the same bytes and statuses.  Set between batches, not

@@ -51,16 +51,20 @@ class GpuCodec:
         return [out[int(oo[i]):int(oo[i]) + int(ol[i])].tobytes() for i in range(n)], st
 
     def decompress(self, comps: list[bytes], caps: list[int], flags: int = 0,
-                   ws_total_in: int | None = None, ws_fill: int | None = None):
+                   ws_total_in: int | None = None, ws_fill: int | None = None, slot_skew: int = 0):
         """ws_total_in: input size the workspace is sized for (default: the
         real packed size; smaller values force the v4 fallback path).
         ws_fill: byte the workspace is filled with before the call (the
-        decoder must not rely on a zeroed workspace)."""
+        decoder must not rely on a zeroed workspace).
+        slot_skew: output slot i starts (i * slot_skew) % 16 bytes past its
+        16-byte-aligned place (slots of every alignment)."""
         torch = self.torch
         b = fsg.Batch.from_list(comps)
         n = len(b)
         caps = np.array(caps, dtype=np.uint32)
-        oo, tot = fsg.slot_offsets(caps.astype(np.uint64))
+        oo, tot = fsg.slot_offsets(caps.astype(np.uint64) + (16 if slot_skew else 0))
+        if slot_skew:
+            oo = oo + (np.arange(n, dtype=np.uint64) * slot_skew) % 16
         d_out = torch.full((max(tot, 1),), POISON, dtype=torch.uint8, device="cuda")
         d_ol = empty(n, torch.int32)
         d_st = torch.full((max(n, 1),), -7, dtype=torch.int32, device="cuda")

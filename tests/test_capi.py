@@ -70,7 +70,7 @@ def test_option_calls():
     lib = fsg.load_gpu_lib()
     names = ["decode_fork", "split_walk", "split_class", "exec_keep", "chunked_huge", "small_persist",
              "small_batch", "split_huge", "walk_order", "lean_walk", "exec_big_blocks", "exec_prio",
-             "exec_big_blocks_fork", "encode_wave_min", "encode_wave_share",
+             "exec_big_blocks_fork", "exec_pack", "encode_wave_min", "encode_wave_share",
              "encode_wave_all_mb", "encode_lanes", "encode_wave_per_cu", "lz4_big_min"]
     v = ctypes.c_int64(0)
     for n in names:

@@ -155,7 +155,7 @@ def test_randomized_against_oracle(gpu, oracle, encoder):
     assert (st == 0).all() and all(o == x for o, x in zip(outs, items))
 
 
-@pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1"), (0, "1p"), (0, "1s0"),
+@pytest.mark.parametrize("variant,fork", [(0, "0"), (3, "0"), (4, "0"), (0, "1"), (0, "1p"), (0, "1k"), (0, "1s0"),
                                           (0, "1s1"), (0, "1s2")])
 def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, fsg_opts):
     """Mutated and truncated streams (64 B to 70 KB bodies).  fork "1" runs
@@ -165,9 +165,12 @@ def test_decode_fuzz_against_oracle(gpu, oracle, variant, fork, fsg_opts):
     ~150 messages (FSG_SMALL_PERSIST); "1sK" with FSG_SPLIT_WALK=K (0: the
     small bodies executed in message order; 1: walk and execution split by
     size on two streams; 2: one execution launch in walk order; default 3:
-    two execution launches by size)."""
+    two execution launches by size); "1k": the smaller bodies packed 32 to a
+    wave (exec_pack 32) instead of one wave each."""
     fsg_opts(decode_fork=fork[0])
     fsg_opts(small_persist="5" if fork == "1p" else "1792")
+    if fork == "1k":
+        fsg_opts(exec_pack=32)
     fsg_opts(split_walk=fork[2] if fork.startswith("1s") else "3")
     gpu.codec.select_kernels(variant, 0)
     rng = np.random.default_rng(9)
@@ -339,7 +342,8 @@ def test_pattern_copies_and_ring_jumps(gpu, oracle, variant):
         gpu.codec.select_kernels(0, 0)
 
 
-def test_small_bodies_forked(gpu, oracle, fsg_opts):
+@pytest.mark.parametrize("pack,skew", [(0, 0), (32, 0), (32, 7), (1, 3), (7, 5), (64, 0)])
+def test_small_bodies_forked(gpu, oracle, pack, skew, fsg_opts):
     """Bodies under 512 compressed bytes on the forked path (the lane walk in
     size-class order + the small bodies' execution): text of every small
     size, hand-built streams (patterns of every offset, COPY_4, 4-byte
@@ -347,8 +351,10 @@ def test_small_bodies_forked(gpu, oracle, fsg_opts):
     single literals, runs with a large output, the reference's negative
     vectors and mutated bodies, trailing zero-length literals -- bytes and
     statuses against the oracle.  (Round 5's one-lane-per-body pass for
-    these, measured slower, was removed in round 6.)"""
-    fsg_opts(decode_fork=1)
+    these, measured slower, was removed in round 6.)  pack: bodies per batch
+    of the packed execution pass (exec_pack; 0 = a wave per body); skew:
+    output slots of every alignment (gpu_harness slot_skew)."""
+    fsg_opts(decode_fork=1, exec_pack=pack)
     rng = np.random.default_rng(77)
     comps = []
     for n in list(range(1, 200, 7)) + list(range(200, 800, 23)):
@@ -380,7 +386,7 @@ def test_small_bodies_forked(gpu, oracle, fsg_opts):
               for n in (3000, 9000, 70000)]
     assert sum(len(c) < 512 for c in comps) > 1000
     caps = [1 << 17] * len(comps)
-    outs, ol, st = gpu.decompress(comps, caps)
+    outs, ol, st = gpu.decompress(comps, caps, slot_skew=skew)
     for i, (c, o, s) in enumerate(zip(comps, outs, st)):
         ok, ulen, ref = oracle.uncompress(c, cap=caps[i])
         if ok is None:

@@ -49,7 +49,7 @@ def main():
     variant = int(os.environ.get("FSG_STAMPS_VARIANT", "5"))
     codec.select_kernels(variant, 0)
     PHASES = PHASES5 if variant == 5 else PHASES4
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 24)()
     codec.decompress(d_c, d_co, d_cl, n, d_out, d_ro, d_rl, d_ol, d_st, workspace=dws)
     torch.cuda.synchronize()
     lib.fsg_debug_stamps(buf, 1)
