@@ -86,7 +86,7 @@ constexpr OptDesc kOptDesc[fsg::kOptCount] = {
     {"exec_big_blocks", "FSG_EXEC_BIG_BLOCKS", 512},
     {"exec_prio", "FSG_EXEC_PRIO", 1},
     {"exec_big_blocks_fork", "FSG_EXEC_BIG_BLOCKS_FORK", 1024},
-    {"exec_pack", "FSG_EXEC_PACK", 0},
+    {"exec_pack", "FSG_EXEC_PACK", 32},
     {"encode_wave_min", "FSG_ENCODE_WAVE_MIN", 16384},
     {"encode_wave_share", "FSG_ENCODE_WAVE_SHARE", 475},
     {"encode_wave_all_mb", "FSG_ENCODE_WAVE_ALL_MB", 640},

@@ -2218,6 +2218,7 @@ __device__ __forceinline__ void exec5_message(
 #endif
 namespace {
 constexpr u32 kFirstTag = 1u << 23;
+constexpr u32 kMidLit = 896;  // literals up to this length run inside a packed group (56 chunks)
 __device__ __forceinline__ u32 lane_bperm(u32 v, u32 src) {
   return (u32)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
@@ -2459,7 +2460,9 @@ __device__ __forceinline__ void exec5_packed(
     const u32 nb = (e >> 16) & 7u;
     const u32 lsrc = pos + 1 + nb;  // body-relative
 
-    const u64 bigm = __ballot(valid && is_lit && len > 64);
+    // literals over kMidLit bytes go straight to the slot (below); shorter
+    // ones over 64 bytes run inside the group, copied by the whole wave
+    const u64 bigm = __ballot(valid && is_lit && len > kMidLit);
     STAMP(1);
     if (bigm & 1ull) {
       // ---------- long literal: straight to the slot by the whole wave; the
@@ -2528,6 +2531,7 @@ __device__ __forceinline__ void exec5_packed(
       if (bad) status[t_m] = kCorrupt;
     }
     const bool run = fits && !bad;
+    const bool mid = run && is_lit && len > 64;  // a literal of 65..kMidLit bytes
 
     // ---------- slide the window if this group would overrun it
     if (op + tot_len - sbase > kWindow) {
@@ -2573,7 +2577,7 @@ __device__ __forceinline__ void exec5_packed(
     const u32 kready = src + len <= op ? nch : (src < op ? (op - src) >> 4 : 0u);
     const u32 klead = kfar > kready ? kfar : kready;
     const u32 kc = pat ? 0u : (klead < nch ? klead : nch);
-    const u32 kf = run ? (is_lit ? nch : kc) : 0u;
+    const u32 kf = run && !mid ? (is_lit ? nch : kc) : 0u;
     const bool reg0 = is_lit && nb == 0;
     const u32 t_oadj = lane_bperm(oadj, tj);
     const u32 sh = is_lit ? (src + t_ioff) & 3u : 0u;
@@ -2597,6 +2601,26 @@ __device__ __forceinline__ void exec5_packed(
     if (kf > 0 && !reg0) gload(0, a0, a0e);
     const u64 m1 = __ballot(kf > 1);
     if (m1 && kf > 1) gload(1, a1, a1e);
+    // the group's first literal over 64 bytes: chunk i by lane i, loaded with
+    // the other round-A loads
+    const u64 ML = __ballot(mid);
+    u32x4 md = u32x4{0, 0, 0, 0};
+    u32 md4 = 0, mcnt = 0, mw = 0, msh = 0;
+    auto mid_load = [&](u32 L0) {
+      const u32 ms = readlane(lsrc, L0) + readlane(t_ioff, L0);
+      const u32 ml = readlane(len, L0);
+      const u32 k = 16 * lane;
+      msh = ms & 3u;
+      mcnt = 0;
+      if (k < ml) {
+        const u32 a = (ms + k) & ~3u;
+        md = __builtin_amdgcn_raw_buffer_load_b128(irsrc, a, 0, 0);
+        md4 = __builtin_amdgcn_raw_buffer_load_b32(irsrc, a + 16, 0, 0);
+        mcnt = ml - k < 16 ? ml - k : 16u;
+        mw = (u32)((int)readlane(t_op, L0) - sbase) + k;
+      }
+    };
+    if (ML) mid_load((u32)__builtin_ctzll(ML));
     prefetch_next_and_zero();
     STAMP(3);
     {
@@ -2615,11 +2639,18 @@ __device__ __forceinline__ void exec5_packed(
         if (kf > 3) or_store(sb, wa + 48, shf(a1, a1e, sh), len - 48, mtab);
       }
     }
+    if (ML) {
+      if (mcnt) or_store(sb, mw, shf(md, md4, msh), mcnt, mtab);
+      for (u64 rest = ML & (ML - 1); rest; rest &= rest - 1) {  // more of them (rare)
+        mid_load((u32)__builtin_ctzll(rest));
+        if (mcnt) or_store(sb, mw, shf(md, md4, msh), mcnt, mtab);
+      }
+    }
     wave_lds_fence();
 
     STAMP(5);
     // ---------- rounds B (as exec5_message)
-    u32 rem = (run && kf < nch) ? len - 16 * kf : 0u;
+    u32 rem = (run && !mid && kf < nch) ? len - 16 * kf : 0u;
     u32 cw = (u32)((int)t_op - sbase) + 16 * kf;
     u32 sw = (u32)((int)src - sbase) + 16 * kf;
     const u32 stp = pat ? pat_step(off) : 16u;
@@ -3231,13 +3262,12 @@ hipError_t launch_decode_v4(const u8* in, const u64* in_off, const u32* in_len,
     return hipGetLastError();
   };
   // The short bodies of walk part 2 packed several to a wave (exec5_packed):
-  // option exec_pack = bodies per batch (1..64; 0, the default = one wave per
+  // option exec_pack = bodies per batch (1..64, default 32; 0 = one wave per
   // body, the small-message grid above).  Grid: the small-message grid's
   // size.  Measured on CM (A/B on one box):
-  // 6.60-6.63 ms at 16/32/64 bodies per batch against 6.11-6.19 with one
-  // wave per body; the packed pass itself ran as long as the wave-per-body
-  // launch it replaces (2.97 vs 2.99 ms) and the side streams beside it
-  // slowed (pass 1b 3.88 -> 4.43 ms).
+  // 5.85-5.92 ms against 6.11-6.19 with one wave per body, once literals of
+  // 65..896 bytes ran inside the group (6.60-6.63 while each was a
+  // wave-wide copy with a window restart).
   const i64 pack_opt = opt(kOptExecPack);
   const u32 kPackBatch = pack_opt >= 1 && pack_opt <= 64 ? (u32)pack_opt : 0u;
   auto launch_packed = [&](hipStream_t st) -> hipError_t {
